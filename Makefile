@@ -1,0 +1,29 @@
+# Build of libsimilarity_transform.so (gfx950) and the CPU oracle.
+# Usage: make [-j16]      (the same recipe __graft_entry__.build() runs)
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fno-fast-math -Wall -Wextra -Wno-unused-parameter -Iinclude \
+            -Ieigen_value_amd/csrc
+SRC      := eigen_value_amd/csrc/st_kernels.hip eigen_value_amd/csrc/st_solve.hip
+OBJ      := $(patsubst eigen_value_amd/csrc/%.hip,build/%.o,$(SRC))
+LIB      := eigen_value_amd/lib/libsimilarity_transform.so
+
+all: $(LIB) oracle
+
+build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(OBJ)
+	@mkdir -p eigen_value_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf build eigen_value_amd/lib
+	$(MAKE) -C oracle clean
+
+.PHONY: all oracle clean

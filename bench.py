@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Benchmark of the similarity-transform round (BASELINE.json `metric`).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--n N0]
+                    [--kind hilbert|random] [--dtype f64|f32] [--no-cpu]
+                    [--no-north-star]
+
+One *step* = one round of the hot path on the HBM-resident matrix: the
+O(N) epilogue (max, eigenvector update, stop test) plus the fused
+scale+row-sum kernel that moves 2*N^2*b bytes (read A_k, write A_{k+1}),
+plus, for N > 1 GPUs, the all-gather of the row-sum vector.  The stop
+tolerance is set to 0 inside the timed region so that every one of the K
+rounds does the full work (after convergence the reference would stop;
+a fixed round count is how SURVEY.md §8d prices ms/iteration).
+
+Workload (config.workload): BASELINE.json configs[1], 8192x8192 Hilbert
+fp64 on one GPU.  For N GPUs the row-block sharded path runs with
+per-GPU bytes held constant (weak scaling): n = 8192*sqrt(N) rounded to a
+multiple of 64*N, rows split in contiguous blocks, one RCCL all-gather per
+round.  `value` = algorithmic bytes of all ranks / max-over-ranks time
+(GB/s); `ms_per_step` = ms/iteration.
+
+Extra objects on the JSON line: `roofline` (fused kernel, HIP events on
+the launch stream), `cpu_baseline` (the CPU oracle's 3-pass schedule on
+the host cores, rank 0 at N=1), `solve` (the reference-semantics solve to
+convergence: rounds, λ), `north_star` (32768x32768 random fp64, 1 GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# fp64 Hilbert 8192, reference semantics (cyclic, EPS=1e-3): 17 rounds,
+# λ = 2.5999921826283514 (CPU oracle; README.md:76 publishes 17 rounds)
+HILBERT8192_F64 = (17, 2.5999921826283514)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--n", type=int, default=8192, help="matrix size at N=1 GPU")
+    p.add_argument("--kind", default="hilbert", choices=["hilbert", "random"])
+    p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    p.add_argument("--no-cpu", action="store_true")
+    p.add_argument("--no-north-star", action="store_true")
+    p.add_argument("--cpu-rounds", type=int, default=5)
+    return p.parse_args()
+
+
+def scaled_n(n1: int, world: int) -> int:
+    if world == 1:
+        return n1
+    q = 64 * world
+    return int(round(n1 * math.sqrt(world) / q)) * q
+
+
+def load_traffic(workload: str):
+    """Per-launch HBM bytes of the fused kernel from committed rocprofv3 PMC
+    passes (profiles/*_pmc.json, written by tools/pmc_traffic.py)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") == workload and d.get("fused_bytes_per_launch"):
+            best = (d["fused_bytes_per_launch"], os.path.relpath(f, HERE))
+    return best
+
+
+def timed_rounds(sh, steps, warmup, torch, dist, world):
+    """Warmup + K timed rounds; returns (elapsed_s_max, fused_ms_avg)."""
+    sh.start()
+    for _ in range(warmup):
+        sh.round(0.0, 2**31)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    p, cur = sh.part, None
+    for k in range(steps):
+        cur = sh.cur
+        s_k = sh.s[cur][:p.n]
+        sh.ops.epilogue(s_k, sh.v, sh.state, 0.0, 2**31, sh.semantics)
+        ev[k][0].record()
+        sh.ops.scale_rowsum(sh.mat, s_k, sh._slot(sh.s[cur ^ 1])[:p.nrows], p.row0,
+                            sh.semantics, sh.state)
+        ev[k][1].record()
+        sh.gather(sh.s[cur ^ 1])
+        sh.cur = cur ^ 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    fused = sum(a.elapsed_time(b) for a, b in ev) / steps
+    if world > 1:
+        t = torch.tensor([el, fused], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el, fused = float(t[0]), float(t[1])
+    return el, fused
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from eigen_value_amd import sharded
+    from eigen_value_amd import _lib
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    _lib.load()   # fail loudly before anything else if the HIP library is missing
+
+    dt = torch.float64 if args.dtype == "f64" else torch.float32
+    b = 8 if args.dtype == "f64" else 4
+    n = scaled_n(args.n, world)
+    workload = f"{args.kind}{n}_{args.dtype}"
+    sh = sharded.ShardedSimilarityTransform(n, dt)
+    p = sh.part
+
+    # ---- reference-semantics solve to convergence (EPS = 1e-3) ----------
+    sh.load(args.kind)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=8)
+    torch.cuda.synchronize()
+    solve_ms = (time.perf_counter() - t0) * 1e3
+    solve = {"eps": 1e-3, "iter_count": iters, "rounds_evaluated": rounds,
+             "eigen_val": lam, "ms": round(solve_ms, 3)}
+    if args.kind == "hilbert" and n == 8192 and args.dtype == "f64":
+        solve["check"] = {"iter_count_expected": HILBERT8192_F64[0],
+                          "eigen_val_rel_err_vs_oracle":
+                              abs(lam - HILBERT8192_F64[1]) / HILBERT8192_F64[1]}
+
+    # ---- timed rounds ----------------------------------------------------
+    sh.load(args.kind, mat=None)
+    el, fused_ms = timed_rounds(sh, args.steps, args.warmup, torch, dist, world)
+    bytes_round_total = 2.0 * n * n * b
+    bytes_round_local = 2.0 * p.nrows * n * b
+    value = bytes_round_total * args.steps / el / 1e9
+    achieved = bytes_round_local / (fused_ms * 1e-3) / 1e9
+    traffic = load_traffic(workload)
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None if traffic is None else traffic[0],
+                "kernel": "k_fused (scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
+                "bytes_per_launch": bytes_round_local,
+                "traffic_source": None if traffic is None else traffic[1]}
+
+    out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
+           "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
+           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": args.dtype, "data": f"synthetic ({args.kind}, generated in HBM)",
+           "config": {"workload": workload, "n": n, "rows_per_gpu": p.chunk,
+                      "bytes_per_round": bytes_round_total, "parallelism": f"rowblock{world}",
+                      "baseline_config": "configs[1]: 8192x8192 Hilbert fp64, 1xMI355X"
+                      if world == 1 else "configs[3]-style row-block sharding, weak-scaled"},
+           "roofline": roofline, "solve": solve}
+    del sh
+    torch.cuda.empty_cache()
+
+    # ---- north-star size: 32768^2 random fp64 on one GPU ---------------
+    if world == 1 and not args.no_north_star:
+        ns = sharded.ShardedSimilarityTransform(32768, torch.float64)
+        ns.load("random", seed=0)
+        lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=4)
+        ns.load("random", seed=0)
+        el_ns, fused_ns = timed_rounds(ns, 20, 3, torch, dist, 1)
+        by = 2.0 * 32768 * 32768 * 8
+        ach = by / (fused_ns * 1e-3) / 1e9
+        tr = load_traffic("random32768_f64")
+        out["north_star"] = {"workload": "random32768_f64", "ms_per_iteration": round(el_ns / 20 * 1e3, 4),
+                             "fused_ms_avg": round(fused_ns, 4), "achieved": round(ach, 1),
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "target_frac": 0.70,
+                             "traffic": None if tr is None else tr[0],
+                             "solve_iter_count": it_ns, "eigen_val": lam_ns}
+        del ns
+        torch.cuda.empty_cache()
+
+    # ---- CPU baseline (rank 0, N = 1) ------------------------------------
+    if world == 1 and rank == 0 and not args.no_cpu:
+        from oracle import oracle as orc
+        threads = min(16, len(os.sched_getaffinity(0)))
+        npdt = np.float64 if args.dtype == "f64" else np.float32
+        mat = orc.hilbert(n, npdt) if args.kind == "hilbert" else orc.random_matrix(n, 0, npdt)
+        r = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=args.cpu_rounds,
+                                     nthreads=threads)
+        # rounds evaluated = cpu_rounds row-sum passes and cpu_rounds-1 transforms;
+        # price it per round with the same 2*N^2*b accounting as `value`
+        per_round_ms = r.loop_ms / args.cpu_rounds
+        out["cpu_baseline"] = {"value": round(bytes_round_total / (per_round_ms * 1e-3) / 1e9, 3),
+                               "unit": "GB/s", "ms_per_iteration": round(per_round_ms, 3),
+                               "cores": threads, "kind": "port",
+                               "sample": f"{workload}, {args.cpu_rounds} rounds (eps=0) of the "
+                                         "reference's 3-pass schedule (oracle/st_oracle.c, gcc "
+                                         "-O3 OpenMP)"}
+        out["speedup_vs_cpu"] = round(out["ms_per_step"] and per_round_ms / out["ms_per_step"], 1)
+
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

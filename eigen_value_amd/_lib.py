@@ -1,0 +1,150 @@
+"""ctypes binding of ``libsimilarity_transform.so`` (include/similarity_transform.h).
+
+The library is built in-tree by ``make`` / ``__graft_entry__.build()`` into
+``eigen_value_amd/lib/``.  There is no fallback: if the shared object is
+missing, every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+DEFAULT_LIB = os.path.join(PKG_DIR, "lib", "libsimilarity_transform.so")
+HEADER = os.path.join(REPO_DIR, "include", "similarity_transform.h")
+
+ST_SEM_SYCL = 0
+ST_SEM_MAINPY = 1
+ST_FLAG_TIME_KERNELS = 1
+ST_MAX_ITR = 1000
+
+DTYPE_F32 = 0
+DTYPE_F64 = 1
+
+
+class EigenValueError(RuntimeError):
+    """A call into libsimilarity_transform.so reported an error."""
+
+
+class st_options(ctypes.Structure):
+    _fields_ = [("eps", ctypes.c_double),
+                ("max_itr", ctypes.c_uint32),
+                ("semantics", ctypes.c_uint32),
+                ("batch", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32)]
+
+
+class st_stats(ctypes.Structure):
+    _fields_ = [("h2d_ms", ctypes.c_double),
+                ("loop_ms", ctypes.c_double),
+                ("d2h_ms", ctypes.c_double),
+                ("fused_ms_total", ctypes.c_double),
+                ("rowsum_ms", ctypes.c_double),
+                ("fused_launches", ctypes.c_uint32),
+                ("rounds", ctypes.c_uint32),
+                ("converged", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
+
+
+class st_state(ctypes.Structure):
+    _fields_ = [("done", ctypes.c_uint32),
+                ("round", ctypes.c_uint32),
+                ("iters", ctypes.c_uint32),
+                ("stop", ctypes.c_uint32),
+                ("lambda_", ctypes.c_double),
+                ("max", ctypes.c_double),
+                ("pad", ctypes.c_uint64 * 4)]
+
+
+assert ctypes.sizeof(st_state) == 64
+assert ctypes.sizeof(st_options) == 24
+assert ctypes.sizeof(st_stats) == 56
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def lib_path() -> str:
+    return os.environ.get("EIGEN_VALUE_LIB", DEFAULT_LIB)
+
+
+def load(path: Optional[str] = None) -> ctypes.CDLL:
+    """Load (once) and declare the C-ABI.  Raises if the .so is missing."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or lib_path()
+    if not os.path.exists(p):
+        raise FileNotFoundError(
+            f"libsimilarity_transform.so not found at {p!r}: run `make` or "
+            "`python -c 'import __graft_entry__ as g; g.build()'` first "
+            "(there is no CPU fallback)")
+    L = ctypes.CDLL(p)
+    _declare(L)
+    if path is None:
+        _lib = L
+    return L
+
+
+def _declare(L: ctypes.CDLL) -> None:
+    P, u32, u64, i32, i64 = (ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                             ctypes.c_int, ctypes.c_int64)
+    f32, f64 = ctypes.c_float, ctypes.c_double
+    L.make_queue.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+    L.make_queue.restype = None
+    L.destroy_queue.argtypes = [P]
+    L.destroy_queue.restype = None
+    L.eigen_last_error.argtypes = []
+    L.eigen_last_error.restype = ctypes.c_char_p
+    L.st_version.restype = ctypes.c_char_p
+    L.st_device_count.restype = i32
+    L.max_eigen_value.argtypes = [P, P, P, P, u32, P]
+    L.max_eigen_value.restype = i64
+    L.max_eigen_value_f64.argtypes = [P, P, P, P, u32, P]
+    L.max_eigen_value_f64.restype = i64
+    L.max_eigen_value_ex.argtypes = [P, i32, P, P, P, u32, P, P, P]
+    L.max_eigen_value_ex.restype = i64
+    L.st_set_stream.argtypes = [P, P]
+    L.st_set_stream.restype = i32
+    for sfx, T in (("f32", f32), ("f64", f64)):
+        fn = getattr(L, f"st_solve_device_{sfx}")
+        fn.argtypes = [P, P, u32, P, P, P, P, P, P]
+        fn.restype = i64
+        getattr(L, f"st_generate_hilbert_{sfx}").argtypes = [P, u32, u32, u32, P]
+        getattr(L, f"st_generate_random_{sfx}").argtypes = [P, u32, u32, u32, u64, P]
+        getattr(L, f"st_generate_identity_{sfx}").argtypes = [P, u32, u32, u32, P]
+        getattr(L, f"st_fill_{sfx}").argtypes = [P, u64, T, P]
+        getattr(L, f"st_rowsum_{sfx}").argtypes = [P, P, u32, u32, P]
+        getattr(L, f"st_scale_rowsum_{sfx}").argtypes = [P, P, P, u32, u32, u32, u32, P, P]
+        getattr(L, f"st_epilogue_{sfx}").argtypes = [P, P, u32, T, u32, u32, P, P]
+        for name in ("generate_hilbert", "generate_random", "generate_identity",
+                     "fill", "rowsum", "scale_rowsum", "epilogue"):
+            getattr(L, f"st_{name}_{sfx}").restype = i32
+    L.st_state_reset.argtypes = [P, P]
+    L.st_state_reset.restype = i32
+
+
+def last_error() -> str:
+    msg = load().eigen_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise EigenValueError(f"{what} failed: {last_error() or 'unknown error'}")
+    return rc
+
+
+def declared_symbols(header: str = HEADER) -> list[str]:
+    """Function names declared inside the extern "C" block of the header."""
+    import re
+    text = open(header).read()
+    body = text.split('extern "C" {', 1)[1].split('} /* extern "C" */', 1)[0]
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", body)
+    skip = {"sizeof"}
+    return sorted({n for n in names if n not in skip and not n.isupper()})

@@ -1,0 +1,338 @@
+// st_device.h — device code of the similarity-transform iteration for
+// gfx950 (CDNA4).  Included by st_kernels.hip (the library) and by
+// tools/tune_fused.hip (launch-shape sweeps); not a public header.
+//
+// Reference behaviour (paths into itzmeanjan/eigen_value):
+//   sum_across_rows       similarity_transform.cpp:77-152
+//   find_max              similarity_transform.cpp:154-227
+//   compute_eigen_vector  similarity_transform.cpp:229-265
+//   compute_next_matrix   similarity_transform.cpp:286-330
+//   stop                  similarity_transform.cpp:332-460
+//   generators            utils.cpp:5-27, 125-154
+//
+// The path is an HBM-bound O(N^2) stream: no MFMA.  One fused kernel per
+// round reads A_k once, writes A_{k+1} = D^-1 A_k D in place and reduces the
+// STORED values into the next round's row sums (the reference sums the
+// stored matrix, similarity_transform.cpp:40,52): 2*N^2*b bytes per round
+// against the reference's 3*N^2*b.  Row sums are reduced without atomics
+// (per-lane running sums in column order -> wave64 shuffle tree -> fixed
+// order LDS combine), so every result is bitwise reproducible.
+//
+// Floating-point contraction must stay off (the stored A_{k+1} element is
+// the rounded product and the sum adds exactly that value): this header
+// sets `#pragma clang fp contract(off)` and the build passes
+// -ffp-contract=off.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "similarity_transform.h"
+
+#pragma clang fp contract(off)
+
+namespace st {
+namespace dev {
+
+constexpr int kBlock = 256; // 4 waves of 64
+constexpr int kWaves = kBlock / 64;
+constexpr int kEpiBlock = 1024; // 16 waves
+
+template <typename T, int W>
+struct vec
+{
+  typedef T type __attribute__((ext_vector_type(W)));
+};
+template <typename T>
+struct vec<T, 1>
+{
+  typedef T type;
+};
+
+template <typename T, int W>
+__device__ __forceinline__ T
+hsum(const typename vec<T, W>::type& y)
+{
+  if constexpr (W == 1) {
+    return y;
+  } else {
+    T t = y[0];
+#pragma unroll
+    for (int k = 1; k < W; k++)
+      t += y[k];
+    return t;
+  }
+}
+
+// fixed tree over the 64 lanes; lane 0 holds the result
+template <typename T>
+__device__ __forceinline__ T
+wave_sum(T x)
+{
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+    x += __shfl_down(x, off, 64);
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T
+wave_max(T x)
+{
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    T y = __shfl_down(x, off, 64);
+    x = y > x ? y : x;
+  }
+  return x;
+}
+
+template <typename V, bool NT>
+__device__ __forceinline__ V
+ld(const V* p)
+{
+  if constexpr (NT)
+    return __builtin_nontemporal_load(p);
+  else
+    return *p;
+}
+
+template <typename V, bool NT>
+__device__ __forceinline__ void
+st(V* p, const V& v)
+{
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+// ---------------------------------------------------------------------------
+// fused scale + row-sum  (plain row-sum when SCALE == false)
+//
+// Workgroup b owns the ROWS consecutive local rows
+// [row_begin + b*ROWS, +ROWS) (always full; the host launches the remainder
+// rows with ROWS = 1) and sweeps their full width, W elements (16 bytes) per
+// lane per access, U column chunks per iteration so that U*ROWS 16-byte
+// loads are in flight per lane.  The column scale s_cur[c] is loaded once
+// per chunk and reused for the ROWS rows.
+// ---------------------------------------------------------------------------
+template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER,
+          bool NT>
+__global__ __launch_bounds__(kBlock) void
+k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+        uint32_t row_begin, uint32_t ncols, uint32_t row0,
+        const st_state* __restrict__ state)
+{
+  using V = typename vec<T, W>::type;
+  if (state != nullptr && state->done)
+    return;
+
+  const uint32_t rbase = row_begin + blockIdx.x * ROWS;
+  const uint32_t nv = ncols / W;
+
+  V* rowp[ROWS];
+  T inv[ROWS];
+  T acc[ROWS];
+#pragma unroll
+  for (int j = 0; j < ROWS; j++) {
+    rowp[j] = reinterpret_cast<V*>(a + (size_t)(rbase + j) * ncols);
+    if constexpr (SCALE)
+      inv[j] = (T)1 / s_cur[row0 + rbase + j];
+    acc[j] = (T)0;
+  }
+  const V* sv = reinterpret_cast<const V*>(s_cur);
+
+  auto body = [&](uint32_t c, auto ucount) {
+    constexpr int UU = decltype(ucount)::value;
+    V x[UU][ROWS];
+    V sc[UU];
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < ROWS; j++)
+        x[u][j] = ld<V, NT>(rowp[j] + c + u * kBlock);
+    if constexpr (SCALE) {
+#pragma unroll
+      for (int u = 0; u < UU; u++)
+        sc[u] = sv[c + u * kBlock];
+#pragma unroll
+      for (int u = 0; u < UU; u++)
+#pragma unroll
+        for (int j = 0; j < ROWS; j++) {
+          if constexpr (ORDER == 0)
+            x[u][j] = x[u][j] * (inv[j] * sc[u]); // sim_transform.cpp:324-325
+          else
+            x[u][j] = (inv[j] * x[u][j]) * sc[u]; // main.py:13-16
+        }
+#pragma unroll
+      for (int u = 0; u < UU; u++)
+#pragma unroll
+        for (int j = 0; j < ROWS; j++)
+          st<V, NT>(rowp[j] + c + u * kBlock, x[u][j]);
+    }
+    if constexpr (SUM) {
+#pragma unroll
+      for (int u = 0; u < UU; u++)
+#pragma unroll
+        for (int j = 0; j < ROWS; j++)
+          acc[j] += hsum<T, W>(x[u][j]);
+    }
+  };
+
+  uint32_t c = threadIdx.x;
+  for (; c + (U - 1) * kBlock < nv; c += U * kBlock)
+    body(c, std::integral_constant<int, U>{});
+  if constexpr (U > 1)
+    for (; c < nv; c += kBlock)
+      body(c, std::integral_constant<int, 1>{});
+
+  if constexpr (SUM) {
+    __shared__ T red[kWaves][ROWS];
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int j = 0; j < ROWS; j++) {
+      T t = wave_sum(acc[j]);
+      if (lane == 0)
+        red[wave][j] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < ROWS) {
+      T t = red[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < kWaves; w++)
+        t += red[w][threadIdx.x];
+      s_next[rbase + threadIdx.x] = t;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// round epilogue: one workgroup over the full row-sum vector
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(kEpiBlock) void
+k_epilogue(const T* __restrict__ s, T* __restrict__ v, uint32_t n, T eps,
+           uint32_t max_itr, uint32_t semantics, st_state* __restrict__ state)
+{
+  if (state->done)
+    return;
+  __shared__ T red[kEpiBlock / 64];
+  __shared__ T m_sh;
+  const bool cyclic = semantics == ST_SEM_SYCL;
+  const uint32_t last = cyclic ? n : n - 1;
+
+  T mx = (T)0; // find_max starts from 0 (similarity_transform.cpp:185)
+  int ok = 1;
+  for (uint32_t i = threadIdx.x; i < n; i += kEpiBlock) {
+    const T x = s[i];
+    mx = x > mx ? x : mx;
+    if (i < last) {
+      const T d = x - s[i + 1 == n ? 0 : i + 1];
+      ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0; // cpp:419-421; NaN fails
+    }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0)
+    red[threadIdx.x >> 6] = mx;
+  const int all_ok = __syncthreads_and(ok);
+  if (threadIdx.x == 0) {
+    T m = red[0];
+    for (int w = 1; w < kEpiBlock / 64; w++)
+      m = red[w] > m ? red[w] : m;
+    m_sh = m;
+  }
+  __syncthreads();
+  const T m = m_sh;
+  if (v != nullptr)
+    for (uint32_t i = threadIdx.x; i < n; i += kEpiBlock)
+      v[i] = v[i] * (s[i] / m); // similarity_transform.cpp:260
+
+  if (threadIdx.x == 0) {
+    const uint32_t i = state->round; // break index if this round stops
+    state->lambda = (double)s[0];    // cpp:60-65
+    state->max = (double)m;
+    state->stop = all_ok ? 1u : 0u;
+    if (all_ok) {
+      state->iters = semantics == ST_SEM_SYCL ? i : i + 1; // cpp:54 / py:47
+      state->done = 1u;
+    } else {
+      state->round = i + 1;
+      if (i + 1 >= max_itr) { // loop exhausted (cpp:39,54)
+        state->iters = max_itr;
+        state->done = 1u;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// generators and fill
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t
+splitmix(uint64_t seed, uint64_t idx)
+{
+  uint64_t z = seed + (idx + 1) * 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+__device__ __forceinline__ T
+uniform01(uint64_t z);
+template <>
+__device__ __forceinline__ double
+uniform01<double>(uint64_t z)
+{
+  return (double)((z >> 11) + 1) * 0x1.0p-53;
+}
+template <>
+__device__ __forceinline__ float
+uniform01<float>(uint64_t z)
+{
+  return (float)((z >> 40) + 1) * 0x1.0p-24f;
+}
+
+enum GenKind
+{
+  kHilbert = 0,
+  kRandom = 1,
+  kIdentity = 2
+};
+
+template <typename T, int KIND>
+__global__ __launch_bounds__(kBlock) void
+k_generate(T* __restrict__ a, uint32_t nrows, uint32_t ncols, uint32_t row0,
+           uint64_t seed)
+{
+  for (uint32_t r = blockIdx.x; r < nrows; r += gridDim.x) {
+    const uint64_t gr = (uint64_t)row0 + r;
+    T* row = a + (size_t)r * ncols;
+    for (uint32_t c = threadIdx.x; c < ncols; c += kBlock) {
+      T x;
+      if constexpr (KIND == kHilbert)
+        x = (T)1 / (T)(gr + c + 1); // utils.cpp:150
+      else if constexpr (KIND == kRandom)
+        x = uniform01<T>(splitmix(seed, gr * ncols + c));
+      else
+        x = (gr == c) ? (T)1 : (T)0; // utils.cpp:5-27
+      row[c] = x;
+    }
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void
+k_fill(T* __restrict__ x, uint64_t count, T value)
+{
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < count;
+       i += (uint64_t)gridDim.x * kBlock)
+    x[i] = value;
+}
+
+} // namespace dev
+} // namespace st

@@ -1,0 +1,48 @@
+// Internal helpers shared by the HIP translation units of
+// libsimilarity_transform.so (not part of the public C-ABI).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "similarity_transform.h"
+
+namespace st {
+
+// thread-local last-error message (eigen_last_error)
+void set_error(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+void clear_error();
+
+#define ST_CHECK(expr)                                                         \
+  do {                                                                         \
+    hipError_t e_ = (expr);                                                    \
+    if (e_ != hipSuccess) {                                                    \
+      ::st::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr,       \
+                      hipGetErrorString(e_));                                  \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)
+
+#define ST_REQUIRE(cond, ...)                                                  \
+  do {                                                                         \
+    if (!(cond)) {                                                             \
+      ::st::set_error(__VA_ARGS__);                                            \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)
+
+// kernel launchers (st_kernels.hip); all asynchronous on `stream`
+template <typename T>
+int launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
+                  hipStream_t stream);
+template <typename T>
+int launch_scale_rowsum(T* a, const T* s_cur, T* s_next, uint32_t nrows,
+                        uint32_t ncols, uint32_t row0, uint32_t semantics,
+                        const st_state* st, hipStream_t stream);
+template <typename T>
+int launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
+                    uint32_t semantics, st_state* st, hipStream_t stream);
+template <typename T>
+int launch_fill(T* x, uint64_t count, T value, hipStream_t stream);
+
+} // namespace st

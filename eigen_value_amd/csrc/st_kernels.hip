@@ -1,0 +1,282 @@
+// st_kernels.hip — launchers for the gfx950 kernels in st_device.h and the
+// step-level C-ABI (similarity_transform.h layer 4).
+//
+// Launch shapes:
+//   fused scale+rowsum / rowsum : 256-thread workgroups, ROWS rows each,
+//                                 16-byte accesses, U chunks in flight;
+//                                 remainder rows (nrows % ROWS) in a second
+//                                 launch with ROWS = 1
+//   epilogue                    : one 1024-thread workgroup
+//   generators / fill           : grid-stride, 256-thread workgroups
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "st_device.h"
+#include "st_internal.h"
+
+namespace st {
+namespace {
+
+using dev::kBlock;
+using dev::kEpiBlock;
+
+inline bool
+aligned16(const void* p)
+{
+  return ((uintptr_t)p & 15u) == 0;
+}
+
+int
+check_launch(const char* what)
+{
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("%s launch failed: %s", what, hipGetErrorString(e));
+    return -1;
+  }
+  return 0;
+}
+
+// Tuned shape of the fused stream (see tools/tune_fused.hip and
+// profiles/): rows per workgroup and column chunks in flight per lane.
+constexpr int kRows = 4;
+constexpr int kUnroll = 2;
+constexpr bool kNontemporal = false;
+
+template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER>
+void
+launch_cfg(T* a, const T* s_cur, T* s_next, uint32_t row_begin,
+           uint32_t nblocks, uint32_t ncols, uint32_t row0,
+           const st_state* st, hipStream_t stream)
+{
+  if (nblocks == 0)
+    return;
+  hipLaunchKernelGGL(
+    (dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, kNontemporal>),
+    dim3(nblocks), dim3(kBlock), 0, stream, a, s_cur, s_next, row_begin, ncols,
+    row0, st);
+}
+
+template <typename T, int W, bool SCALE, bool SUM, int ORDER>
+void
+launch_rows(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
+            uint32_t row0, const st_state* st, hipStream_t stream)
+{
+  // small matrices: one row per workgroup keeps >= 256 workgroups busy
+  if (nrows < 2048) {
+    launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(a, s_cur, s_next, 0, nrows,
+                                                    ncols, row0, st, stream);
+    return;
+  }
+  const uint32_t full = nrows / kRows;
+  launch_cfg<T, kRows, W, kUnroll, SCALE, SUM, ORDER>(
+    a, s_cur, s_next, 0, full, ncols, row0, st, stream);
+  launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(
+    a, s_cur, s_next, full * kRows, nrows - full * kRows, ncols, row0, st,
+    stream);
+}
+
+template <typename T, bool SCALE, bool SUM, int ORDER>
+void
+launch_vec(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
+           uint32_t row0, const st_state* st, hipStream_t stream)
+{
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok =
+    (ncols % W) == 0 && aligned16(a) && (!SCALE || aligned16(s_cur));
+  if (vec_ok)
+    launch_rows<T, W, SCALE, SUM, ORDER>(a, s_cur, s_next, nrows, ncols, row0,
+                                         st, stream);
+  else
+    launch_rows<T, 1, SCALE, SUM, ORDER>(a, s_cur, s_next, nrows, ncols, row0,
+                                         st, stream);
+}
+
+} // namespace
+
+template <typename T>
+int
+launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
+              hipStream_t stream)
+{
+  ST_REQUIRE(a && s, "rowsum: null pointer");
+  if (nrows == 0)
+    return 0;
+  ST_REQUIRE(ncols > 0, "rowsum: ncols must be > 0");
+  launch_vec<T, false, true, 0>(const_cast<T*>(a), nullptr, s, nrows, ncols, 0,
+                                nullptr, stream);
+  return check_launch("rowsum");
+}
+
+template <typename T>
+int
+launch_scale_rowsum(T* a, const T* s_cur, T* s_next, uint32_t nrows,
+                    uint32_t ncols, uint32_t row0, uint32_t semantics,
+                    const st_state* st, hipStream_t stream)
+{
+  ST_REQUIRE(a && s_cur, "scale_rowsum: null pointer");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "scale_rowsum: bad semantics %u",
+             semantics);
+  if (nrows == 0)
+    return 0;
+  ST_REQUIRE(ncols > 0, "scale_rowsum: ncols must be > 0");
+  const bool order1 = semantics == ST_SEM_MAINPY;
+  if (s_next) {
+    if (order1)
+      launch_vec<T, true, true, 1>(a, s_cur, s_next, nrows, ncols, row0, st,
+                                   stream);
+    else
+      launch_vec<T, true, true, 0>(a, s_cur, s_next, nrows, ncols, row0, st,
+                                   stream);
+  } else {
+    if (order1)
+      launch_vec<T, true, false, 1>(a, s_cur, nullptr, nrows, ncols, row0, st,
+                                    stream);
+    else
+      launch_vec<T, true, false, 0>(a, s_cur, nullptr, nrows, ncols, row0, st,
+                                    stream);
+  }
+  return check_launch("scale_rowsum");
+}
+
+template <typename T>
+int
+launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
+                uint32_t semantics, st_state* st, hipStream_t stream)
+{
+  ST_REQUIRE(s && st, "epilogue: null pointer");
+  ST_REQUIRE(n > 0, "epilogue: n must be > 0");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "epilogue: bad semantics %u",
+             semantics);
+  hipLaunchKernelGGL(dev::k_epilogue<T>, dim3(1), dim3(kEpiBlock), 0, stream,
+                     s, v, n, eps, max_itr, semantics, st);
+  return check_launch("epilogue");
+}
+
+template <typename T>
+int
+launch_fill(T* x, uint64_t count, T value, hipStream_t stream)
+{
+  ST_REQUIRE(x || count == 0, "fill: null pointer");
+  if (count == 0)
+    return 0;
+  uint64_t blocks = (count + kBlock - 1) / kBlock;
+  const uint32_t grid = (uint32_t)(blocks < 8192 ? blocks : 8192);
+  hipLaunchKernelGGL(dev::k_fill<T>, dim3(grid), dim3(kBlock), 0, stream, x,
+                     count, value);
+  return check_launch("fill");
+}
+
+template <typename T, int KIND>
+int
+launch_generate(T* a, uint32_t nrows, uint32_t ncols, uint32_t row0,
+                uint64_t seed, hipStream_t stream)
+{
+  ST_REQUIRE(a || nrows == 0 || ncols == 0, "generate: null pointer");
+  if (nrows == 0 || ncols == 0)
+    return 0;
+  const uint32_t grid = nrows < 65536 ? nrows : 65536;
+  hipLaunchKernelGGL((dev::k_generate<T, KIND>), dim3(grid), dim3(kBlock), 0,
+                     stream, a, nrows, ncols, row0, seed);
+  return check_launch("generate");
+}
+
+template int launch_rowsum<float>(const float*, float*, uint32_t, uint32_t,
+                                  hipStream_t);
+template int launch_rowsum<double>(const double*, double*, uint32_t, uint32_t,
+                                   hipStream_t);
+template int launch_scale_rowsum<float>(float*, const float*, float*, uint32_t,
+                                        uint32_t, uint32_t, uint32_t,
+                                        const st_state*, hipStream_t);
+template int launch_scale_rowsum<double>(double*, const double*, double*,
+                                         uint32_t, uint32_t, uint32_t,
+                                         uint32_t, const st_state*,
+                                         hipStream_t);
+template int launch_epilogue<float>(const float*, float*, uint32_t, float,
+                                    uint32_t, uint32_t, st_state*,
+                                    hipStream_t);
+template int launch_epilogue<double>(const double*, double*, uint32_t, double,
+                                     uint32_t, uint32_t, st_state*,
+                                     hipStream_t);
+template int launch_fill<float>(float*, uint64_t, float, hipStream_t);
+template int launch_fill<double>(double*, uint64_t, double, hipStream_t);
+
+} // namespace st
+
+// ---------------------------------------------------------------------------
+// step-level C-ABI (similarity_transform.h, layer 4)
+// ---------------------------------------------------------------------------
+#define ST_STREAM(p) (reinterpret_cast<hipStream_t>(p))
+
+extern "C" {
+
+int
+st_state_reset(st_state* d_state, void* stream)
+{
+  st::clear_error();
+  ST_REQUIRE(d_state, "st_state_reset: null state");
+  ST_CHECK(hipMemsetAsync(d_state, 0, sizeof(st_state), ST_STREAM(stream)));
+  return 0;
+}
+
+#define ST_STEP_EXPORTS(T, SFX)                                                \
+  int st_generate_hilbert_##SFX(T* d_mat, unsigned int nrows,                  \
+                                unsigned int ncols, unsigned int row0,         \
+                                void* stream)                                  \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_generate<T, st::dev::kHilbert>(d_mat, nrows, ncols,      \
+                                                     row0, 0,                  \
+                                                     ST_STREAM(stream));       \
+  }                                                                            \
+  int st_generate_random_##SFX(T* d_mat, unsigned int nrows,                   \
+                               unsigned int ncols, unsigned int row0,          \
+                               uint64_t seed, void* stream)                    \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_generate<T, st::dev::kRandom>(d_mat, nrows, ncols, row0, \
+                                                    seed, ST_STREAM(stream));  \
+  }                                                                            \
+  int st_generate_identity_##SFX(T* d_mat, unsigned int nrows,                 \
+                                 unsigned int ncols, unsigned int row0,        \
+                                 void* stream)                                 \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_generate<T, st::dev::kIdentity>(                         \
+      d_mat, nrows, ncols, row0, 0, ST_STREAM(stream));                        \
+  }                                                                            \
+  int st_fill_##SFX(T* d_x, uint64_t count, T value, void* stream)             \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_fill<T>(d_x, count, value, ST_STREAM(stream));           \
+  }                                                                            \
+  int st_rowsum_##SFX(const T* d_mat, T* d_s, unsigned int nrows,              \
+                      unsigned int ncols, void* stream)                        \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_rowsum<T>(d_mat, d_s, nrows, ncols, ST_STREAM(stream)); \
+  }                                                                            \
+  int st_scale_rowsum_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,           \
+                            unsigned int nrows, unsigned int ncols,            \
+                            unsigned int row0, unsigned int semantics,         \
+                            const st_state* d_state, void* stream)             \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_scale_rowsum<T>(d_mat, d_s_cur, d_s_next, nrows, ncols,  \
+                                      row0, semantics, d_state,                \
+                                      ST_STREAM(stream));                      \
+  }                                                                            \
+  int st_epilogue_##SFX(const T* d_s, T* d_v, unsigned int n, T eps,           \
+                        unsigned int max_itr, unsigned int semantics,          \
+                        st_state* d_state, void* stream)                       \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_epilogue<T>(d_s, d_v, n, eps, max_itr, semantics,        \
+                                  d_state, ST_STREAM(stream));                 \
+  }
+
+ST_STEP_EXPORTS(float, f32)
+ST_STEP_EXPORTS(double, f64)
+
+} // extern "C"

@@ -1,0 +1,486 @@
+// st_solve.hip — host orchestration of the similarity-transform round loop
+// and the drop-in C-ABI (similarity_transform.h layers 1-3).
+//
+// Replaces, in the reference (itzmeanjan/eigen_value):
+//   wrapper/similarity_transform.cpp:3-37   make_queue / max_eigen_value
+//   similarity_transform.cpp:5-75           similarity_transform() host loop
+//
+// Round loop (one device stream, no per-round host sync):
+//   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
+//   per round k:
+//     K2  epilogue(s_k): max, v *= s/m, stop test, lambda = s_k[0]
+//     K1  A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})
+//         (skipped on device once K2 has set done)
+// The reference blocks on a host_accessor every round
+// (similarity_transform.cpp:45-50).  Here rounds are enqueued in batches;
+// the host checks the device `done` flag of batch b while batch b+1 is
+// already queued, and rounds after convergence are device-gated no-ops, so
+// the observable results (lambda, v, iter_count) are exactly those of the
+// sequential loop.
+
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "st_internal.h"
+
+namespace st {
+
+static thread_local char g_err[512];
+
+void
+set_error(const char* fmt, ...)
+{
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+void
+clear_error()
+{
+  g_err[0] = '\0';
+}
+
+namespace {
+
+constexpr uint32_t kDefaultBatch = 8;
+
+struct Context
+{
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr; // own_stream or a caller stream
+  // cached device workspaces (grown on demand, freed by destroy_queue)
+  void* d_mat = nullptr;
+  size_t mat_bytes = 0;
+  void* d_vec = nullptr; // [s0 | s1 | v], each vec_bytes
+  size_t vec_bytes = 0;
+  st_state* d_state = nullptr;
+  st_state* h_state = nullptr; // pinned, 2 slots
+  hipEvent_t ev_flag[2] = { nullptr, nullptr };
+};
+
+double
+ms_since(std::chrono::steady_clock::time_point t0)
+{
+  return std::chrono::duration<double, std::milli>(
+           std::chrono::steady_clock::now() - t0)
+    .count();
+}
+
+int
+ensure_device(Context* c)
+{
+  ST_CHECK(hipSetDevice(c->device));
+  return 0;
+}
+
+int
+ensure_vectors(Context* c, size_t vec_bytes)
+{
+  vec_bytes = (vec_bytes + 255) & ~(size_t)255;
+  if (c->d_vec && c->vec_bytes >= vec_bytes)
+    return 0;
+  if (c->d_vec) {
+    ST_CHECK(hipStreamSynchronize(c->stream));
+    ST_CHECK(hipFree(c->d_vec));
+    c->d_vec = nullptr;
+  }
+  ST_CHECK(hipMalloc(&c->d_vec, 3 * vec_bytes));
+  c->vec_bytes = vec_bytes;
+  return 0;
+}
+
+int
+ensure_matrix(Context* c, size_t bytes)
+{
+  if (c->d_mat && c->mat_bytes >= bytes)
+    return 0;
+  if (c->d_mat) {
+    ST_CHECK(hipStreamSynchronize(c->stream));
+    ST_CHECK(hipFree(c->d_mat));
+    c->d_mat = nullptr;
+    c->mat_bytes = 0;
+  }
+  ST_CHECK(hipMalloc(&c->d_mat, bytes));
+  c->mat_bytes = bytes;
+  return 0;
+}
+
+template <typename T>
+T
+default_eps();
+template <>
+float
+default_eps<float>()
+{
+  return ST_EPS_F32; // include/similarity_transform.hpp:4 (float)
+}
+template <>
+double
+default_eps<double>()
+{
+  return ST_EPS_F64; // main.py:6
+}
+
+struct Resolved
+{
+  double eps;
+  uint32_t max_itr, semantics, batch, flags;
+};
+
+template <typename T>
+int
+resolve(const st_options* opt, Resolved* r)
+{
+  r->eps = (opt && opt->eps >= 0.0) ? opt->eps : (double)default_eps<T>();
+  r->max_itr = (opt && opt->max_itr) ? opt->max_itr : ST_MAX_ITR;
+  r->semantics = opt ? opt->semantics : ST_SEM_SYCL;
+  r->batch = (opt && opt->batch) ? opt->batch : kDefaultBatch;
+  r->flags = opt ? opt->flags : 0u;
+  ST_REQUIRE(r->semantics <= ST_SEM_MAINPY, "unknown semantics %u",
+             r->semantics);
+  return 0;
+}
+
+// The round loop on a device-resident matrix (transformed in place).
+template <typename T>
+int64_t
+solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
+             T* eigen_val, uint32_t* iter_cnt, const st_options* opt,
+             st_stats* stats)
+{
+  ST_REQUIRE(c, "null queue");
+  ST_REQUIRE(d_mat, "null matrix");
+  ST_REQUIRE(n > 0, "dim must be > 0");
+  ST_REQUIRE(eigen_val && iter_cnt, "null output pointer");
+  ST_REQUIRE(d_v_out || v_host, "need a device or host eigenvector output");
+  Resolved o;
+  if (resolve<T>(opt, &o))
+    return -1;
+  if (ensure_device(c) || ensure_vectors(c, sizeof(T) * (size_t)n))
+    return -1;
+  hipStream_t s = c->stream;
+  T* s_buf[2] = { reinterpret_cast<T*>(c->d_vec),
+                  reinterpret_cast<T*>((char*)c->d_vec + c->vec_bytes) };
+  T* d_v = d_v_out ? d_v_out
+                   : reinterpret_cast<T*>((char*)c->d_vec + 2 * c->vec_bytes);
+  const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
+  std::vector<hipEvent_t> ev; // [rowsum_a, rowsum_b, (k1_a, k1_b)*]
+  auto mk = [&](hipEvent_t* e) -> int {
+    ST_CHECK(hipEventCreate(e));
+    return 0;
+  };
+  int rc = 0;
+  auto cleanup = [&]() {
+    for (hipEvent_t e : ev)
+      if (e)
+        (void)hipEventDestroy(e);
+  };
+
+  const auto t0 = std::chrono::steady_clock::now();
+  ST_CHECK(hipMemsetAsync(c->d_state, 0, sizeof(st_state), s));
+  if (launch_fill<T>(d_v, n, (T)1, s)) // initialise_eigen_vector, cpp:34
+    return -1;
+  if (timed) {
+    ev.resize(2, nullptr);
+    if (mk(&ev[0]) || mk(&ev[1])) {
+      cleanup();
+      return -1;
+    }
+    (void)hipEventRecord(ev[0], s);
+  }
+  if (launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) { // K0
+    cleanup();
+    return -1;
+  }
+  if (timed)
+    (void)hipEventRecord(ev[1], s);
+
+  const T eps = (T)o.eps;
+  uint32_t enqueued = 0, cur = 0, batch_no = 0;
+  bool done = false;
+  while (!done && enqueued < o.max_itr) {
+    const uint32_t b = (o.max_itr - enqueued) < o.batch ? (o.max_itr - enqueued)
+                                                        : o.batch;
+    for (uint32_t k = 0; k < b; k++) {
+      rc |= launch_epilogue<T>(s_buf[cur], d_v, n, eps, o.max_itr, o.semantics,
+                               c->d_state, s);
+      hipEvent_t ea = nullptr, eb = nullptr;
+      if (timed) {
+        rc |= mk(&ea) | mk(&eb);
+        ev.push_back(ea);
+        ev.push_back(eb);
+        (void)hipEventRecord(ea, s);
+      }
+      rc |= launch_scale_rowsum<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], n, n, 0,
+                                   o.semantics, c->d_state, s);
+      if (timed)
+        (void)hipEventRecord(eb, s);
+      cur ^= 1;
+      if (rc) {
+        cleanup();
+        return -1;
+      }
+    }
+    enqueued += b;
+    const int slot = batch_no & 1;
+    ST_CHECK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(st_state),
+                            hipMemcpyDeviceToHost, s));
+    ST_CHECK(hipEventRecord(c->ev_flag[slot], s));
+    // wait for the previous batch's flag while this batch runs
+    if (batch_no > 0) {
+      ST_CHECK(hipEventSynchronize(c->ev_flag[slot ^ 1]));
+      done = c->h_state[slot ^ 1].done != 0;
+    }
+    batch_no++;
+  }
+  ST_CHECK(hipStreamSynchronize(s));
+  const double loop_ms = ms_since(t0);
+  st_state fin;
+  ST_CHECK(hipMemcpy(&fin, c->d_state, sizeof(st_state), hipMemcpyDeviceToHost));
+  ST_REQUIRE(fin.done, "internal: loop ended without done flag");
+
+  const auto t1 = std::chrono::steady_clock::now();
+  *eigen_val = (T)fin.lambda;
+  *iter_cnt = fin.iters;
+  if (v_host)
+    ST_CHECK(hipMemcpy(v_host, d_v, sizeof(T) * (size_t)n,
+                       hipMemcpyDeviceToHost));
+  const double d2h_ms = ms_since(t1);
+
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->loop_ms = loop_ms;
+    stats->d2h_ms = d2h_ms;
+    stats->rounds = fin.stop ? fin.round + 1 : fin.round;
+    stats->converged = fin.stop;
+    if (timed) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+      stats->rowsum_ms = ms;
+      // transforms actually executed: rounds that did not stop, minus the
+      // device-skipped one at max_itr
+      uint32_t transforms = fin.stop ? fin.round
+                                     : (fin.round > 0 ? fin.round - 1 : 0);
+      double tot = 0.0;
+      for (uint32_t k = 0; k < transforms && 2 + 2 * k + 1 < ev.size(); k++) {
+        (void)hipEventElapsedTime(&ms, ev[2 + 2 * k], ev[2 + 2 * k + 1]);
+        tot += ms;
+      }
+      stats->fused_ms_total = tot;
+      stats->fused_launches = transforms;
+    }
+  }
+  cleanup();
+  return (int64_t)loop_ms;
+}
+
+template <typename T>
+int64_t
+solve_host(Context* c, const T* mat, uint32_t n, T* eigen_val, T* eigen_vec,
+           uint32_t* iter_cnt, const st_options* opt, st_stats* stats)
+{
+  ST_REQUIRE(c, "null queue");
+  ST_REQUIRE(mat && eigen_val && eigen_vec && iter_cnt, "null pointer");
+  ST_REQUIRE(n > 0, "dim must be > 0");
+  if (ensure_device(c))
+    return -1;
+  const size_t bytes = sizeof(T) * (size_t)n * n;
+  if (ensure_matrix(c, bytes))
+    return -1;
+  // the reference's timed region starts before the first kernel, which
+  // performs the lazy host->device copy (similarity_transform.cpp:36-40)
+  const auto t0 = std::chrono::steady_clock::now();
+  ST_CHECK(hipMemcpyAsync(c->d_mat, mat, bytes, hipMemcpyHostToDevice,
+                          c->stream));
+  ST_CHECK(hipStreamSynchronize(c->stream));
+  const double h2d = ms_since(t0);
+  st_stats local{};
+  if (solve_device<T>(c, reinterpret_cast<T*>(c->d_mat), n, nullptr,
+                      eigen_vec, eigen_val, iter_cnt, opt, &local) < 0)
+    return -1;
+  local.h2d_ms = h2d;
+  if (stats)
+    *stats = local;
+  return (int64_t)(h2d + local.loop_ms);
+}
+
+Context*
+as_ctx(void* wq)
+{
+  return reinterpret_cast<Context*>(wq);
+}
+
+} // namespace
+} // namespace st
+
+using st::Context;
+
+extern "C" {
+
+const char*
+eigen_last_error(void)
+{
+  return st::g_err;
+}
+
+const char*
+st_version(void)
+{
+  return "eigen_value_amd 0.1.0 (gfx950)";
+}
+
+int
+st_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess)
+    return 0;
+  return n;
+}
+
+void
+make_queue(void** wq)
+{
+  st::clear_error();
+  if (!wq)
+    return;
+  *wq = nullptr;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) {
+    st::set_error("make_queue: no HIP device");
+    return;
+  }
+  if (const char* e = std::getenv("EIGEN_VALUE_DEVICE"))
+    dev = std::atoi(e);
+  Context* c = new (std::nothrow) Context();
+  if (!c) {
+    st::set_error("make_queue: out of host memory");
+    return;
+  }
+  c->device = dev;
+  bool ok = hipSetDevice(dev) == hipSuccess &&
+            hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) ==
+              hipSuccess &&
+            hipMalloc(&c->d_state, sizeof(st_state)) == hipSuccess &&
+            hipHostMalloc(&c->h_state, 2 * sizeof(st_state),
+                          hipHostMallocDefault) == hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_flag[0], hipEventDisableTiming) ==
+              hipSuccess &&
+            hipEventCreateWithFlags(&c->ev_flag[1], hipEventDisableTiming) ==
+              hipSuccess;
+  if (!ok) {
+    st::set_error("make_queue: HIP initialisation failed: %s",
+                  hipGetErrorString(hipGetLastError()));
+    destroy_queue(c);
+    return;
+  }
+  c->stream = c->own_stream;
+  *wq = c;
+}
+
+void
+destroy_queue(void* wq)
+{
+  Context* c = st::as_ctx(wq);
+  if (!c)
+    return;
+  (void)hipSetDevice(c->device);
+  if (c->stream)
+    (void)hipStreamSynchronize(c->stream);
+  if (c->d_mat)
+    (void)hipFree(c->d_mat);
+  if (c->d_vec)
+    (void)hipFree(c->d_vec);
+  if (c->d_state)
+    (void)hipFree(c->d_state);
+  if (c->h_state)
+    (void)hipHostFree(c->h_state);
+  for (hipEvent_t e : c->ev_flag)
+    if (e)
+      (void)hipEventDestroy(e);
+  if (c->own_stream)
+    (void)hipStreamDestroy(c->own_stream);
+  delete c;
+}
+
+int
+st_set_stream(void* wq, void* stream)
+{
+  st::clear_error();
+  Context* c = st::as_ctx(wq);
+  ST_REQUIRE(c, "st_set_stream: null queue");
+  c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own_stream;
+  return 0;
+}
+
+int64_t
+max_eigen_value(void* wq, float* mat, float* eigen_val, float* eigen_vec,
+                unsigned int dim, unsigned int* iter_cnt)
+{
+  st::clear_error();
+  return st::solve_host<float>(st::as_ctx(wq), mat, dim, eigen_val, eigen_vec,
+                               iter_cnt, nullptr, nullptr);
+}
+
+int64_t
+max_eigen_value_f64(void* wq, double* mat, double* eigen_val,
+                    double* eigen_vec, unsigned int dim,
+                    unsigned int* iter_cnt)
+{
+  st::clear_error();
+  return st::solve_host<double>(st::as_ctx(wq), mat, dim, eigen_val,
+                                eigen_vec, iter_cnt, nullptr, nullptr);
+}
+
+int64_t
+max_eigen_value_ex(void* wq, int dtype, const void* mat, void* eigen_val,
+                   void* eigen_vec, unsigned int dim, unsigned int* iter_cnt,
+                   const st_options* opt, st_stats* stats)
+{
+  st::clear_error();
+  if (dtype == 0)
+    return st::solve_host<float>(st::as_ctx(wq), (const float*)mat, dim,
+                                 (float*)eigen_val, (float*)eigen_vec,
+                                 iter_cnt, opt, stats);
+  if (dtype == 1)
+    return st::solve_host<double>(st::as_ctx(wq), (const double*)mat, dim,
+                                  (double*)eigen_val, (double*)eigen_vec,
+                                  iter_cnt, opt, stats);
+  st::set_error("max_eigen_value_ex: dtype must be 0 (f32) or 1 (f64)");
+  return -1;
+}
+
+int64_t
+st_solve_device_f32(void* wq, float* d_mat, unsigned int dim,
+                    float* d_eigen_vec, float* eigen_vec_host,
+                    float* eigen_val, unsigned int* iter_cnt,
+                    const st_options* opt, st_stats* stats)
+{
+  st::clear_error();
+  return st::solve_device<float>(st::as_ctx(wq), d_mat, dim, d_eigen_vec,
+                                 eigen_vec_host, eigen_val, iter_cnt, opt,
+                                 stats);
+}
+
+int64_t
+st_solve_device_f64(void* wq, double* d_mat, unsigned int dim,
+                    double* d_eigen_vec, double* eigen_vec_host,
+                    double* eigen_val, unsigned int* iter_cnt,
+                    const st_options* opt, st_stats* stats)
+{
+  st::clear_error();
+  return st::solve_device<double>(st::as_ctx(wq), d_mat, dim, d_eigen_vec,
+                                  eigen_vec_host, eigen_val, iter_cnt, opt,
+                                  stats);
+}
+
+} // extern "C"

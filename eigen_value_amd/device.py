@@ -1,0 +1,191 @@
+"""Device-resident API over torch-ROCm tensors.
+
+Torch is plumbing here (HBM allocation, streams); every kernel is the HIP
+code in ``libsimilarity_transform.so`` launched through the C-ABI on the
+caller's current torch stream.  Nothing in this module computes on the CPU:
+a missing library raises, a non-CUDA tensor raises.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+from . import _lib
+
+_SFX = {}
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _sfx(t) -> str:
+    torch = _torch()
+    if t.dtype == torch.float64:
+        return "f64"
+    if t.dtype == torch.float32:
+        return "f32"
+    raise TypeError(f"float32/float64 tensor required, got {t.dtype}")
+
+
+def _check_cuda(*ts) -> None:
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise ValueError("device API needs tensors on a HIP device (cuda:N)")
+
+
+def _stream(device=None) -> int:
+    torch = _torch()
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _ptr(t) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+# --------------------------------------------------------------------------
+# state
+# --------------------------------------------------------------------------
+def new_state(device="cuda"):
+    """A zeroed 64-byte ``st_state`` on the device (uint8 tensor)."""
+    torch = _torch()
+    return torch.zeros(64, dtype=torch.uint8, device=device)
+
+
+def reset_state(state) -> None:
+    _check_cuda(state)
+    _lib.check(_lib.load().st_state_reset(_ptr(state), _stream(state.device)), "st_state_reset")
+
+
+def read_state(state) -> dict:
+    raw = bytes(state.cpu().numpy().tobytes())
+    s = _lib.st_state.from_buffer_copy(raw)
+    return dict(done=s.done, round=s.round, iters=s.iters, stop=s.stop,
+                eigen_val=s.lambda_, max=s.max)
+
+
+# --------------------------------------------------------------------------
+# generators
+# --------------------------------------------------------------------------
+def generate(kind: str, n: int, dtype=None, nrows: Optional[int] = None, row0: int = 0,
+             seed: int = 0, device="cuda", out=None):
+    """Rows [row0, row0+nrows) of an n-wide input matrix generated on device.
+
+    kind: 'hilbert' (utils.cpp:137-154), 'random' (seeded splitmix64 U(0,1]),
+    'identity' (utils.cpp:5-27)."""
+    torch = _torch()
+    dtype = dtype or torch.float64
+    nrows = n if nrows is None else nrows
+    if out is None:
+        out = torch.empty((nrows, n), dtype=dtype, device=device)
+    _check_cuda(out)
+    L, sfx, st = _lib.load(), _sfx(out), _stream(out.device)
+    if kind == "hilbert":
+        rc = getattr(L, f"st_generate_hilbert_{sfx}")(_ptr(out), nrows, n, row0, st)
+    elif kind == "random":
+        rc = getattr(L, f"st_generate_random_{sfx}")(_ptr(out), nrows, n, row0, seed, st)
+    elif kind == "identity":
+        rc = getattr(L, f"st_generate_identity_{sfx}")(_ptr(out), nrows, n, row0, st)
+    else:
+        raise ValueError(f"unknown generator {kind!r}")
+    _lib.check(rc, f"generate_{kind}")
+    return out
+
+
+def fill(x, value: float) -> None:
+    _check_cuda(x)
+    _lib.check(getattr(_lib.load(), f"st_fill_{_sfx(x)}")(_ptr(x), x.numel(), value,
+                                                          _stream(x.device)), "fill")
+
+
+# --------------------------------------------------------------------------
+# step-level kernels
+# --------------------------------------------------------------------------
+def rowsum(mat, out=None):
+    """s[r] = Σ_c A[r][c] for the rows of ``mat`` (sum_across_rows)."""
+    _check_cuda(mat)
+    assert mat.is_contiguous() and mat.dim() == 2
+    if out is None:
+        out = mat.new_empty(mat.shape[0])
+    _lib.check(getattr(_lib.load(), f"st_rowsum_{_sfx(mat)}")(
+        _ptr(mat), _ptr(out), mat.shape[0], mat.shape[1], _stream(mat.device)), "rowsum")
+    return out
+
+
+def scale_rowsum(mat, s_cur, s_next=None, row0: int = 0,
+                 semantics: int = _lib.ST_SEM_SYCL, state=None) -> None:
+    """Fused round body, in place on ``mat`` (local rows row0..): see
+    ``st_scale_rowsum_*`` in include/similarity_transform.h."""
+    _check_cuda(mat, s_cur, s_next, state)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    assert s_cur.numel() >= ncols and s_cur.numel() >= row0 + nrows
+    if s_next is not None:
+        assert s_next.numel() >= nrows
+    _lib.check(getattr(_lib.load(), f"st_scale_rowsum_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(s_next), nrows, ncols, row0, semantics,
+        _ptr(state), _stream(mat.device)), "scale_rowsum")
+
+
+def epilogue(s, v, state, eps: float, max_itr: int = _lib.ST_MAX_ITR,
+             semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """Round epilogue: max, v *= s/m, stop test, λ = s[0], bookkeeping."""
+    _check_cuda(s, v, state)
+    _lib.check(getattr(_lib.load(), f"st_epilogue_{_sfx(s)}")(
+        _ptr(s), _ptr(v), s.numel(), eps, max_itr, semantics, _ptr(state),
+        _stream(s.device)), "epilogue")
+
+
+# --------------------------------------------------------------------------
+# whole solve on a device-resident matrix
+# --------------------------------------------------------------------------
+class DeviceSolver:
+    """Owns one library context bound to the current torch stream."""
+
+    def __init__(self, device=None):
+        torch = _torch()
+        self.device = torch.device(device or "cuda")
+        self.L = _lib.load()
+        with torch.cuda.device(self.device):
+            self.q = ctypes.c_void_p()
+            self.L.make_queue(ctypes.byref(self.q))
+        if not self.q.value:
+            raise _lib.EigenValueError(f"make_queue failed: {_lib.last_error()}")
+
+    def solve(self, mat, *, inplace: bool = False, eps: Optional[float] = None,
+              max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL, batch: int = 0,
+              time_kernels: bool = False):
+        """Returns (λ: float, v: tensor, iterations: int, stats: dict).
+
+        ``mat`` is transformed in place when ``inplace`` (it is the private
+        working copy the reference makes, similarity_transform.cpp:14,19)."""
+        torch = _torch()
+        _check_cuda(mat)
+        n = mat.shape[0]
+        assert mat.shape == (n, n), "must be square"
+        work = mat if inplace else mat.clone()
+        work = work.contiguous()
+        v = torch.empty(n, dtype=mat.dtype, device=mat.device)
+        ev = (ctypes.c_double if mat.dtype == torch.float64 else ctypes.c_float)()
+        it = ctypes.c_uint32()
+        opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
+                              batch, _lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
+        stats = _lib.st_stats()
+        _lib.check(self.L.st_set_stream(self.q, _stream(mat.device)), "st_set_stream")
+        rc = getattr(self.L, f"st_solve_device_{_sfx(mat)}")(
+            self.q, _ptr(work), n, _ptr(v), None, ctypes.byref(ev), ctypes.byref(it),
+            ctypes.byref(opt), ctypes.byref(stats))
+        _lib.check(rc, "st_solve_device")
+        return float(ev.value), v, int(it.value), stats.as_dict()
+
+    def close(self) -> None:
+        if self.q is not None and self.q.value:
+            self.L.destroy_queue(self.q)
+            self.q = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,179 @@
+"""Row-block sharded round loop over ``torch.distributed`` (RCCL on MI355X).
+
+North-star layout (BASELINE.json): for N beyond one GPU's HBM, rank p of P
+owns the contiguous rows ``[p*chunk, p*chunk + nrows_p)`` of A, with
+``chunk = ceil(N/P)``.  Per round:
+
+1. local fused kernel: ``A_p <- D^-1 A_p D`` (needs the FULL s_k for the
+   column scale) and ``s_{k+1}[local rows]``;
+2. ONE all-gather of the N-length row-sum vector (N*b/P bytes in per rank);
+3. every rank runs the O(N) epilogue redundantly on the identical gathered
+   vector (max, eigenvector, cyclic stop, λ) — deterministic kernels on
+   bitwise-identical input, so all ranks agree on ``done`` without a
+   further collective.
+
+The reference has no distributed code at all ("Parallelism
+strategies ... none"); this is the exchange north_star asks for.  The
+per-shard compute is pluggable (``ops``): ``HipShardOps`` runs the HIP
+kernels through the C-ABI; tests substitute a CPU stand-in to exercise the
+partition / gather / bookkeeping logic with the gloo backend.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+from . import _lib
+
+
+@dataclass(frozen=True)
+class RowBlock:
+    n: int
+    world: int
+    rank: int
+    chunk: int      # padded rows per rank (gather slot size)
+    row0: int       # first global row owned
+    nrows: int      # rows owned (<= chunk; the last ranks may own fewer)
+
+
+def row_block(n: int, world: int, rank: int) -> RowBlock:
+    if n <= 0 or world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad partition n={n} world={world} rank={rank}")
+    chunk = math.ceil(n / world)
+    row0 = min(rank * chunk, n)
+    nrows = max(0, min(n, row0 + chunk) - row0)
+    return RowBlock(n, world, rank, chunk, row0, nrows)
+
+
+class HipShardOps:
+    """Per-shard steps on the GPU (libsimilarity_transform.so)."""
+
+    def __init__(self, device=None):
+        import torch
+        from . import device as dev
+        self.torch, self.dev = torch, dev
+        self.device = torch.device(device or "cuda")
+
+    def empty(self, shape, dtype):
+        return self.torch.empty(shape, dtype=dtype, device=self.device)
+
+    def generate(self, kind, n, dtype, nrows, row0, seed):
+        return self.dev.generate(kind, n, dtype=dtype, nrows=nrows, row0=row0,
+                                 seed=seed, device=self.device)
+
+    def new_state(self):
+        return self.dev.new_state(self.device)
+
+    def reset_state(self, state):
+        self.dev.reset_state(state)
+
+    def fill(self, x, value):
+        self.dev.fill(x, value)
+
+    def rowsum(self, mat, out):
+        if mat.shape[0]:
+            self.dev.rowsum(mat, out=out)
+
+    def scale_rowsum(self, mat, s_cur, s_next, row0, semantics, state):
+        if mat.shape[0]:
+            self.dev.scale_rowsum(mat, s_cur, s_next, row0=row0,
+                                  semantics=semantics, state=state)
+
+    def epilogue(self, s, v, state, eps, max_itr, semantics):
+        self.dev.epilogue(s, v, state, eps, max_itr, semantics)
+
+    def read_state(self, state) -> dict:
+        return self.dev.read_state(state)
+
+
+def _allgather(out, inp, group=None):
+    """out[rank*chunk:(rank+1)*chunk] <- inp on every rank (in-place safe)."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "gloo":
+        world = dist.get_world_size(group)
+        parts = list(out.chunk(world))
+        dist.all_gather(parts, inp.clone(), group=group)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+class ShardedSimilarityTransform:
+    """The round loop of similarity_transform.cpp:34-66 over P row blocks."""
+
+    def __init__(self, n: int, dtype=None, group=None, ops=None,
+                 semantics: int = _lib.ST_SEM_SYCL):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group = torch, dist, group
+        self.dtype = dtype or torch.float64
+        self.n = n
+        self.semantics = semantics
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.part = row_block(n, world, rank)
+        self.ops = ops or HipShardOps()
+        p = self.part
+        self.s = [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(2)]
+        self.v = self.ops.empty((n,), self.dtype)
+        self.state = self.ops.new_state()
+        self.mat = None
+
+    # local slot of a gathered vector
+    def _slot(self, s):
+        p = self.part
+        return s[p.rank * p.chunk:(p.rank + 1) * p.chunk]
+
+    def load(self, kind: str = "hilbert", seed: int = 0, mat=None):
+        """Generate (or adopt) this rank's row block."""
+        p = self.part
+        if mat is not None:
+            assert tuple(mat.shape) == (p.nrows, p.n)
+            self.mat = mat
+        else:
+            self.mat = self.ops.generate(kind, p.n, self.dtype, p.nrows, p.row0, seed)
+        return self.mat
+
+    def gather(self, s):
+        if self.part.world > 1:
+            _allgather(s, self._slot(s), self.group)
+
+    def start(self):
+        """v = 1, state = 0, s_0 = rowsum(A_0) gathered (K0)."""
+        p = self.part
+        self.ops.reset_state(self.state)
+        self.ops.fill(self.v, 1.0)
+        self.ops.rowsum(self.mat, self._slot(self.s[0])[:p.nrows])
+        self.gather(self.s[0])
+        self.cur = 0
+
+    def round(self, eps: float, max_itr: int):
+        """One round: epilogue(s_k) then fused transform + row sums + gather."""
+        p, cur = self.part, self.cur
+        s_k = self.s[cur][:p.n]
+        self.ops.epilogue(s_k, self.v, self.state, eps, max_itr, self.semantics)
+        self.ops.scale_rowsum(self.mat, s_k, self._slot(self.s[cur ^ 1])[:p.nrows],
+                              p.row0, self.semantics, self.state)
+        self.gather(self.s[cur ^ 1])
+        self.cur = cur ^ 1
+
+    def solve(self, eps: Optional[float] = None, max_itr: int = _lib.ST_MAX_ITR,
+              batch: int = 4):
+        """Run to convergence; returns (λ, v, iterations, rounds_evaluated)."""
+        if eps is None:
+            eps = 1e-3
+        self.start()
+        enqueued = 0
+        while enqueued < max_itr:
+            b = min(batch, max_itr - enqueued)
+            for _ in range(b):
+                self.round(eps, max_itr)
+            enqueued += b
+            st = self.ops.read_state(self.state)   # synchronises this rank
+            if st["done"]:
+                break
+        st = self.ops.read_state(self.state)
+        if not st["done"]:
+            raise _lib.EigenValueError("sharded solve ended without done flag")
+        rounds = st["round"] + 1 if st["stop"] else st["round"]
+        return st["eigen_val"], self.v, st["iters"], rounds

@@ -1,0 +1,248 @@
+/*
+ * similarity_transform.h — C-ABI of libsimilarity_transform.so, the
+ * MI355X (gfx950) implementation of the similarity-transform maximum
+ * eigenvalue iteration.
+ *
+ * Plain C: pointers, sizes, no torch or HIP types in any signature
+ * (streams are passed as `void*` = hipStream_t).  Citations refer to the
+ * reference tree (itzmeanjan/eigen_value), path:line.
+ *
+ * Layers
+ *   1. Drop-in exports: exactly the two symbols the reference's Python
+ *      wrapper binds (wrapper/python/similarity_transform.py:33-37,63-69).
+ *   2. Additions at the same level (fp64 twin, queue teardown, last error,
+ *      an extended call with options and statistics).
+ *   3. Device-resident solve (input already in HBM; bench and torch users).
+ *   4. Step-level kernels on a caller stream: what the row-block sharded
+ *      driver (eigen_value_amd/sharded.py) and the kernel unit tests call.
+ *
+ * Errors: nothing throws across this ABI.  Functions returning int64_t /
+ * int return a negative value on error and record a message readable with
+ * eigen_last_error() (thread-local).  make_queue writes NULL on failure.
+ *
+ * Threading: a queue (context) is used by one host thread at a time.
+ */
+#ifndef EIGEN_VALUE_AMD_SIMILARITY_TRANSFORM_H
+#define EIGEN_VALUE_AMD_SIMILARITY_TRANSFORM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* include/similarity_transform.hpp:4-5 */
+#define ST_EPS_F32 1e-3f
+#define ST_EPS_F64 1e-3
+#define ST_MAX_ITR 1000u
+
+/* semantics of the round loop */
+#define ST_SEM_SYCL 0u   /* similarity_transform.cpp: cyclic stop (413-417),   */
+                         /* A *= (1/s_r)*s_c (324-325), count = break idx (54) */
+#define ST_SEM_MAINPY 1u /* main.py: non-cyclic stop (25-27),                 */
+                         /* ((1/s_r)*A)*s_c (13-16), count = itr + 1 (47)     */
+
+/* ---------------------------------------------------------------------- */
+/* 1. drop-in exports                                                      */
+/* ---------------------------------------------------------------------- */
+
+/* replaces wrapper/similarity_transform.cpp:3-12 (sycl::default_selector
+ * queue).  Creates a context on the current HIP device (env
+ * EIGEN_VALUE_DEVICE overrides) with its own non-blocking stream.
+ * *wq = NULL on failure. */
+void make_queue(void** wq);
+
+/* replaces wrapper/similarity_transform.cpp:14-37 and, behind it,
+ * similarity_transform.cpp:5-75.  fp32, reference semantics (ST_SEM_SYCL,
+ * EPS = 1e-3f, MAX_ITR = 1000).  `mat` (dim x dim, row-major) is read only.
+ * Writes eigen_val[0], eigen_vec[0..dim), *iter_cnt.  Returns elapsed ms
+ * (steady clock, host->device copy of `mat` included, as the reference's
+ * lazily-copied buffer is) or a negative value on error.  Any dim >= 1 is
+ * accepted (the reference required dim % work-group-size == 0). */
+int64_t max_eigen_value(void* wq, float* mat, float* eigen_val,
+                        float* eigen_vec, unsigned int dim,
+                        unsigned int* iter_cnt);
+
+/* ---------------------------------------------------------------------- */
+/* 2. additions                                                            */
+/* ---------------------------------------------------------------------- */
+
+/* fp64 twin of max_eigen_value (EPS = 1e-3). */
+int64_t max_eigen_value_f64(void* wq, double* mat, double* eigen_val,
+                            double* eigen_vec, unsigned int dim,
+                            unsigned int* iter_cnt);
+
+/* Frees a context from make_queue (the reference leaks its queue). */
+void destroy_queue(void* wq);
+
+/* Message of the last error on this thread ("" if none). */
+const char* eigen_last_error(void);
+
+typedef struct st_options
+{
+  double eps;         /* stop tolerance; < 0 selects the dtype default     */
+  uint32_t max_itr;   /* 0 selects ST_MAX_ITR                               */
+  uint32_t semantics; /* ST_SEM_SYCL or ST_SEM_MAINPY                       */
+  uint32_t batch;     /* rounds enqueued per host flag check; 0 = default   */
+  uint32_t flags;     /* ST_FLAG_* below                                    */
+} st_options;
+
+#define ST_FLAG_TIME_KERNELS 1u /* hipEvents around every fused launch     */
+
+typedef struct st_stats
+{
+  double h2d_ms;          /* host->device copy of the input               */
+  double loop_ms;         /* first kernel .. convergence observed on host */
+  double d2h_ms;          /* eigenvector / eigenvalue copy back           */
+  double fused_ms_total;  /* sum of fused scale+rowsum kernel times       */
+  double rowsum_ms;       /* the initial row-sum pass                     */
+  uint32_t fused_launches;/* fused launches timed                         */
+  uint32_t rounds;        /* row-sum evaluations performed                */
+  uint32_t converged;     /* 1 if the stop test passed before max_itr     */
+  uint32_t reserved;
+} st_stats;
+
+/* Extended host-pointer solve.  dtype: 0 = float32, 1 = float64.
+ * opt / stats may be NULL. */
+int64_t max_eigen_value_ex(void* wq, int dtype, const void* mat,
+                           void* eigen_val, void* eigen_vec,
+                           unsigned int dim, unsigned int* iter_cnt,
+                           const st_options* opt, st_stats* stats);
+
+/* Make the context launch on a caller stream (hipStream_t; NULL restores
+ * the context's own stream).  Returns 0 or negative. */
+int st_set_stream(void* wq, void* stream);
+
+/* ---------------------------------------------------------------------- */
+/* 3. device-resident solve                                                */
+/* ---------------------------------------------------------------------- */
+
+/* d_mat: device pointer, dim x dim row-major; TRANSFORMED IN PLACE (it is
+ * the private working copy the reference makes at
+ * similarity_transform.cpp:14,19).  d_eigen_vec: device pointer [dim] or
+ * NULL (then eigen_vec_host must be non-NULL and receives it).
+ * eigen_val / iter_cnt: host pointers.  Returns loop ms or negative. */
+int64_t st_solve_device_f32(void* wq, float* d_mat, unsigned int dim,
+                            float* d_eigen_vec, float* eigen_vec_host,
+                            float* eigen_val, unsigned int* iter_cnt,
+                            const st_options* opt, st_stats* stats);
+int64_t st_solve_device_f64(void* wq, double* d_mat, unsigned int dim,
+                            double* d_eigen_vec, double* eigen_vec_host,
+                            double* eigen_val, unsigned int* iter_cnt,
+                            const st_options* opt, st_stats* stats);
+
+/* ---------------------------------------------------------------------- */
+/* 4. step-level kernels (asynchronous on `stream`, a hipStream_t or NULL) */
+/* ---------------------------------------------------------------------- */
+
+/* Device state of one solve (64 bytes, zero = fresh). */
+typedef struct st_state
+{
+  uint32_t done;   /* 1 once the stop test passed or max_itr was reached  */
+  uint32_t round;  /* row-sum evaluations that did not stop               */
+  uint32_t iters;  /* reference iter_count, valid once done               */
+  uint32_t stop;   /* stop flag of the last evaluated round               */
+  double lambda;   /* s[0] of the last evaluated round                    */
+  double max;      /* max row sum of the last evaluated round             */
+  uint64_t pad[4];
+} st_state;
+
+/* zero a state (hipMemsetAsync) */
+int st_state_reset(st_state* d_state, void* stream);
+
+/* inputs for rows [row0, row0+nrows) of an ncols-wide matrix:
+ *   hilbert  A[r][c] = 1/(r+c+1) in the element type (utils.cpp:137-154)
+ *   random   U(0,1] from splitmix64(seed, r*ncols+c) (replaces the
+ *            non-reproducible utils.cpp:125-134)
+ *   identity (utils.cpp:5-27), fill (constant value) */
+int st_generate_hilbert_f32(float* d_mat, unsigned int nrows,
+                            unsigned int ncols, unsigned int row0,
+                            void* stream);
+int st_generate_hilbert_f64(double* d_mat, unsigned int nrows,
+                            unsigned int ncols, unsigned int row0,
+                            void* stream);
+int st_generate_random_f32(float* d_mat, unsigned int nrows,
+                           unsigned int ncols, unsigned int row0,
+                           uint64_t seed, void* stream);
+int st_generate_random_f64(double* d_mat, unsigned int nrows,
+                           unsigned int ncols, unsigned int row0,
+                           uint64_t seed, void* stream);
+int st_generate_identity_f32(float* d_mat, unsigned int nrows,
+                             unsigned int ncols, unsigned int row0,
+                             void* stream);
+int st_generate_identity_f64(double* d_mat, unsigned int nrows,
+                             unsigned int ncols, unsigned int row0,
+                             void* stream);
+int st_fill_f32(float* d_x, uint64_t count, float value, void* stream);
+int st_fill_f64(double* d_x, uint64_t count, double value, void* stream);
+
+/* s[r] = sum_c A[r][c] for the nrows local rows (similarity_transform.cpp
+ * :77-152, deterministic tree order, no atomics). */
+int st_rowsum_f32(const float* d_mat, float* d_s, unsigned int nrows,
+                  unsigned int ncols, void* stream);
+int st_rowsum_f64(const double* d_mat, double* d_s, unsigned int nrows,
+                  unsigned int ncols, void* stream);
+
+/* Fused round body: for the local rows r in [0,nrows) (global row0 + r),
+ *   A[r][c] = A[r][c] * ((1/s_cur[row0+r]) * s_cur[c])     (ST_SEM_SYCL)
+ *   A[r][c] = ((1/s_cur[row0+r]) * A[r][c]) * s_cur[c]     (ST_SEM_MAINPY)
+ * in place (similarity_transform.cpp:286-330 / main.py:13-16), and
+ * s_next[r] = sum_c of the stored A[r][c] (the next round's row sums,
+ * similarity_transform.cpp:40).  s_next may be NULL (transform only).
+ * d_state may be NULL; otherwise the launch is a no-op once done != 0. */
+int st_scale_rowsum_f32(float* d_mat, const float* d_s_cur, float* d_s_next,
+                        unsigned int nrows, unsigned int ncols,
+                        unsigned int row0, unsigned int semantics,
+                        const st_state* d_state, void* stream);
+int st_scale_rowsum_f64(double* d_mat, const double* d_s_cur,
+                        double* d_s_next, unsigned int nrows,
+                        unsigned int ncols, unsigned int row0,
+                        unsigned int semantics, const st_state* d_state,
+                        void* stream);
+
+/* Round epilogue on the full row-sum vector s[0..n): m = max(0, max s)
+ * (find_max, similarity_transform.cpp:154-227), v[i] *= s[i]/m
+ * (compute_eigen_vector, :229-265), stop = all |s[i]-s[i+1]| < eps over
+ * the cyclic (ST_SEM_SYCL, :332-460) or open (ST_SEM_MAINPY) pairs,
+ * lambda = s[0]; then done/round/iters bookkeeping against max_itr.
+ * No-op once done != 0.  d_v may be NULL (no eigenvector update). */
+int st_epilogue_f32(const float* d_s, float* d_v, unsigned int n, float eps,
+                    unsigned int max_itr, unsigned int semantics,
+                    st_state* d_state, void* stream);
+int st_epilogue_f64(const double* d_s, double* d_v, unsigned int n,
+                    double eps, unsigned int max_itr, unsigned int semantics,
+                    st_state* d_state, void* stream);
+
+/* Library / device facts. */
+const char* st_version(void);
+int st_device_count(void);
+
+#ifdef __cplusplus
+} /* extern "C" */
+
+/* C++ entry mirroring include/similarity_transform.hpp:46-53
+ * (int64_t similarity_transform(sycl::queue&, const float* mat, float*
+ * eigen_val, float* eigen_vec, uint dim, uint wg_size, uint* iter_count)).
+ * The queue becomes the opaque context; wg_size is accepted and ignored
+ * (tiles are chosen by the kernels). */
+inline int64_t
+similarity_transform(void* q, const float* mat, float* const eigen_val,
+                     float* const eigen_vec, const unsigned int dim,
+                     const unsigned int /*wg_size*/,
+                     unsigned int* const iter_count)
+{
+  return max_eigen_value_ex(q, 0, mat, eigen_val, eigen_vec, dim, iter_count,
+                            nullptr, nullptr);
+}
+inline int64_t
+similarity_transform(void* q, const double* mat, double* const eigen_val,
+                     double* const eigen_vec, const unsigned int dim,
+                     const unsigned int /*wg_size*/,
+                     unsigned int* const iter_count)
+{
+  return max_eigen_value_ex(q, 1, mat, eigen_val, eigen_vec, dim, iter_count,
+                            nullptr, nullptr);
+}
+#endif
+
+#endif /* EIGEN_VALUE_AMD_SIMILARITY_TRANSFORM_H */

@@ -1,0 +1,94 @@
+"""CPU: the C-ABI library loads and exports every symbol the header declares;
+host-side wrapper logic.  No compute calls (no GPU here)."""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from eigen_value_amd import _lib
+
+
+def test_library_exists_and_loads():
+    assert os.path.exists(_lib.lib_path()), "run `make` first"
+    L = _lib.load()
+    assert L.st_version().decode().startswith("eigen_value_amd")
+
+
+def test_exports_every_declared_symbol():
+    declared = _lib.declared_symbols()
+    # the two drop-in names bound by wrapper/python/similarity_transform.py
+    assert "make_queue" in declared and "max_eigen_value" in declared
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()],
+                         capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [s for s in declared if s not in exported]
+    assert not missing, missing
+    L = _lib.load()
+    for s in declared:
+        assert getattr(L, s) is not None
+
+
+def test_drop_in_signatures_are_c_abi():
+    # extern "C" names are unmangled; the drop-in pair keeps the reference's
+    # argument list (wrapper/similarity_transform.cpp:3-37)
+    hdr = open(_lib.HEADER).read()
+    assert "void make_queue(void** wq);" in hdr
+    assert ("int64_t max_eigen_value(void* wq, float* mat, float* eigen_val,\n"
+            "                        float* eigen_vec, unsigned int dim,\n"
+            "                        unsigned int* iter_cnt);") in hdr
+
+
+def test_struct_layouts():
+    assert ctypes.sizeof(_lib.st_state) == 64
+    assert ctypes.sizeof(_lib.st_options) == 24
+    assert ctypes.sizeof(_lib.st_stats) == 56
+
+
+def test_no_device_errors_are_clean():
+    L = _lib.load()
+    if L.st_device_count() > 0:
+        pytest.skip("a GPU is present")
+    q = ctypes.c_void_p(123)
+    L.make_queue(ctypes.byref(q))
+    assert q.value is None
+    assert "no HIP device" in _lib.last_error()
+    # NULL queue -> negative return + message, never a crash
+    m = np.ones((4, 4), np.float32)
+    ev, vec, it = np.zeros(1, np.float32), np.zeros(4, np.float32), np.zeros(1, np.uint32)
+    rc = L.max_eigen_value(None, m.ctypes.data, ev.ctypes.data, vec.ctypes.data, 4, it.ctypes.data)
+    assert rc < 0 and "null queue" in _lib.last_error()
+    with pytest.raises(Exception, match="queue"):
+        import eigen_value_amd
+        eigen_value_amd.EigenValue()
+
+
+def test_step_api_argument_errors():
+    L = _lib.load()
+    assert L.st_rowsum_f64(None, None, 4, 4, None) < 0
+    assert "null" in _lib.last_error()
+    assert L.st_epilogue_f32(None, None, 0, 1e-3, 10, 0, None, None) < 0
+    assert L.st_scale_rowsum_f64(None, None, None, 4, 4, 0, 7, None, None) < 0
+    # zero-sized work is a no-op, not an error
+    assert L.st_fill_f64(None, 0, 1.0, None) == 0
+
+
+def test_missing_library_raises(monkeypatch, tmp_path):
+    monkeypatch.setenv("EIGEN_VALUE_LIB", str(tmp_path / "nope.so"))
+    with pytest.raises(FileNotFoundError, match="no CPU fallback"):
+        _lib.load(_lib.lib_path())
+
+
+def test_header_compiles_as_c_and_cxx(tmp_path):
+    src_c = tmp_path / "t.c"
+    src_c.write_text('#include "similarity_transform.h"\nint main(void){return (int)sizeof(st_state)-64;}\n')
+    inc = os.path.dirname(_lib.HEADER)
+    subprocess.run(["gcc", "-std=c11", "-Wall", "-Werror", f"-I{inc}", str(src_c), "-o", str(tmp_path / "tc")], check=True)
+    src_cc = tmp_path / "t.cc"
+    src_cc.write_text('#include "similarity_transform.h"\n'
+                      'int main(){ int64_t (*f)(void*, const double*, double*, double*,\n'
+                      '  unsigned, unsigned, unsigned*) = &similarity_transform;\n'
+                      '  return f ? (int)sizeof(st_options)-24 : 1; }\n')
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", f"-I{inc}", "-c", str(src_cc),
+                    "-o", str(tmp_path / "tcc.o")], check=True)

@@ -1,0 +1,297 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Tolerances (stated here):
+  * generators, the D^-1 A D element update: BIT-exact;
+  * fp64 solves vs the oracle with the same semantics: iteration count equal,
+    λ relative <= 1e-10, eigenvector max-abs <= 1e-10 (summation order
+    differs: tree on the GPU, numpy pairwise in the oracle);
+  * fp64 ST_SEM_MAINPY solves vs the reference's main.py golden vectors:
+    iteration count equal, λ relative <= 1e-12, eigenvector max-abs <= 1e-12;
+  * fp32: iteration counts equal to the reference's published counts
+    (README.md:70-76), λ relative <= 1e-5.
+"""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no HIP device", allow_module_level=True)
+
+import eigen_value_amd as ev  # noqa: E402
+from eigen_value_amd import _lib  # noqa: E402
+from eigen_value_amd import device as dev  # noqa: E402
+from conftest import golden_input  # noqa: E402
+
+DEV = "cuda:0"
+TD = {np.float64: torch.float64, np.float32: torch.float32}
+
+
+@pytest.fixture(scope="module")
+def eigen():
+    e = ev.EigenValue()
+    yield e
+    e.close()
+
+
+@pytest.fixture(scope="module")
+def solver():
+    s = dev.DeviceSolver(DEV)
+    yield s
+    s.close()
+
+
+def to_np(t):
+    torch.cuda.synchronize()
+    return t.cpu().numpy()
+
+
+# ---------------------------------------------------------------------------
+# generators
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("n,nrows,row0", [(1, 1, 0), (7, 7, 0), (130, 17, 33), (1000, 3, 997)])
+def test_generators_bitexact(orc, dt, n, nrows, row0):
+    h = dev.generate("hilbert", n, TD[dt], nrows=nrows, row0=row0, device=DEV)
+    assert np.array_equal(to_np(h), orc.hilbert(n, dt, nrows=nrows, row0=row0))
+    r = dev.generate("random", n, TD[dt], nrows=nrows, row0=row0, seed=42, device=DEV)
+    assert np.array_equal(to_np(r), orc.random_matrix(n, 42, dt, nrows=nrows, row0=row0))
+    i = dev.generate("identity", n, TD[dt], nrows=nrows, row0=row0, device=DEV)
+    assert np.array_equal(to_np(i), np.eye(n, dtype=dt)[row0:row0 + nrows])
+
+
+# ---------------------------------------------------------------------------
+# per-kernel pins: tests/test.cpp:22-73
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_kernel_unit_pins(dt):
+    n = 1024
+    eye = dev.generate("identity", n, TD[dt], device=DEV)
+    assert np.all(to_np(dev.rowsum(eye)) == 1.0)                 # test.cpp:22-30
+    s = torch.arange(1, n + 1, dtype=TD[dt], device=DEV)
+    v = torch.ones(n, dtype=TD[dt], device=DEV)
+    state = dev.new_state(DEV)
+    dev.epilogue(s, v, state, eps=1e-3, max_itr=1000)
+    st = dev.read_state(state)
+    assert st["max"] == n                                          # test.cpp:32-41
+    assert np.max(np.abs(to_np(s) / n - to_np(v))) == 0.0         # test.cpp:43-54
+    assert st["stop"] == 0 and st["done"] == 0 and st["round"] == 1
+    ok = torch.full((n,), float(np.float32(1) + np.float32(1e-4)), dtype=TD[dt], device=DEV)
+    dev.reset_state(state)
+    dev.epilogue(ok, None, state, eps=1e-3)
+    assert dev.read_state(state)["stop"] == 1                      # test.cpp:56-64
+    fail = (torch.arange(n, dtype=TD[dt], device=DEV) + 1) * float(np.float32(1e-4))
+    dev.reset_state(state)
+    dev.epilogue(fail, None, state, eps=1e-3)
+    assert dev.read_state(state)["stop"] == 0                      # test.cpp:66-73 (cyclic)
+    dev.reset_state(state)
+    dev.epilogue(fail, None, state, eps=1e-3, semantics=_lib.ST_SEM_MAINPY)
+    assert dev.read_state(state)["stop"] == 1                      # main.py:25-27
+
+
+# ---------------------------------------------------------------------------
+# row sums and the fused round body
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("nrows,ncols", [(1, 1), (5, 3), (37, 1001), (2051, 256), (4100, 515), (64, 8192)])
+def test_rowsum_vs_oracle(orc, dt, nrows, ncols):
+    a = orc.random_matrix(ncols, 7, dt, nrows=nrows)
+    got = to_np(dev.rowsum(torch.from_numpy(a).to(DEV)))
+    ref = orc.rowsum(a)
+    tol = 1e-13 if dt == np.float64 else 2e-6
+    assert np.max(np.abs(got - ref) / np.abs(ref)) <= tol
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
+@pytest.mark.parametrize("nrows,ncols,row0", [(3, 3, 0), (64, 257, 100), (2050, 4096, 1000), (4099, 4100, 1)])
+def test_fused_step_vs_oracle(orc, dt, sem, nrows, ncols, row0):
+    n_full = max(ncols, row0 + nrows)
+    a = orc.random_matrix(ncols, 3, dt, nrows=nrows)
+    s_full = (orc.random_matrix(n_full, 9, dt, nrows=1)[0] + dt(0.5)).astype(dt)
+    ta = torch.from_numpy(a).to(DEV)
+    ts = torch.from_numpy(s_full).to(DEV)
+    s_next = torch.empty(nrows, dtype=TD[dt], device=DEV)
+    dev.scale_rowsum(ta, ts, s_next, row0=row0, semantics=sem)
+    got = to_np(ta)
+    ref = orc.compute_next(a, s_full, row0=row0, order=0 if sem == _lib.ST_SEM_SYCL else 1)
+    assert np.array_equal(got, ref)                    # element update is bit-exact
+    ref_s = orc.rowsum(ref)
+    tol = 1e-13 if dt == np.float64 else 2e-6
+    assert np.max(np.abs(to_np(s_next) - ref_s) / np.abs(ref_s)) <= tol
+
+
+def test_fused_step_is_gated_by_done(orc):
+    a = orc.random_matrix(300, 1)
+    ta = torch.from_numpy(a).to(DEV)
+    s = torch.full((300,), 2.0, dtype=torch.float64, device=DEV)
+    state = dev.new_state(DEV)
+    # mark done: epilogue on a constant vector stops immediately
+    dev.epilogue(s, None, state, eps=1e-3)
+    assert dev.read_state(state)["done"] == 1
+    dev.scale_rowsum(ta, s * 3.0, torch.empty_like(s), state=state)
+    assert np.array_equal(to_np(ta), a)
+
+
+def test_row_sums_independent_of_partition(orc):
+    # per-row reduction order does not depend on ROWS / launch split, so a
+    # row block gives bitwise the same sums as the full matrix
+    a = orc.random_matrix(3000, 5)
+    full = to_np(dev.rowsum(torch.from_numpy(a).to(DEV)))
+    part = to_np(dev.rowsum(torch.from_numpy(a[1234:1240]).to(DEV)))
+    assert np.array_equal(full[1234:1240], part)
+
+
+# ---------------------------------------------------------------------------
+# whole solves through the drop-in API
+# ---------------------------------------------------------------------------
+def test_dropin_kat3(eigen, golden):
+    kat = golden[2]["kat3"]
+    lam, v, ts, itr = eigen.similarity_transform(np.array(kat["matrix"], dtype=np.float32))
+    assert isinstance(lam, np.float32) and v.dtype == np.float32 and ts >= 0
+    assert abs(lam - kat["eigen_val"]) < kat["tol"]                # test.cpp:99
+    assert np.all(np.abs(v - np.array(kat["eigen_vec"])) < kat["tol"])
+    assert itr == 4
+
+
+def test_dropin_hilbert_round_counts_fp32(eigen, orc, golden):
+    p = golden[2]["hilbert_round_counts_fp32"]
+    for n, rounds in zip(p["sizes"], p["rounds"]):
+        mat = orc.hilbert(n, np.float32)
+        lam, v, ts, itr = eigen.similarity_transform(mat)
+        assert itr == rounds, (n, itr, rounds)                     # README.md:70-76
+        ref = orc.similarity_transform(mat, orc.SEM_SYCL)
+        assert abs(lam - ref.eigen_val) <= 1e-5 * ref.eigen_val
+        assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-4
+
+
+@pytest.mark.parametrize("kind,n", [("hilbert", 128), ("hilbert", 1000), ("hilbert", 4096),
+                                    ("random", 333), ("random", 1024), ("random", 4099)])
+def test_dropin_fp64_vs_oracle(eigen, orc, kind, n):
+    mat = orc.hilbert(n) if kind == "hilbert" else orc.random_matrix(n, 11)
+    lam, v, ts, itr = eigen.similarity_transform(mat)
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL)
+    assert isinstance(lam, np.float64)
+    assert itr == ref.iter_count
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
+
+
+def test_mainpy_semantics_vs_reference_golden(eigen, orc, golden):
+    cases, vecs, _ = golden
+    for name, case in cases.items():
+        mat = golden_input(case, orc)
+        lam, v, ts, itr, stats = eigen.similarity_transform_ex(mat, semantics=_lib.ST_SEM_MAINPY)
+        assert itr == case["itr"], name
+        assert abs(lam - case["eigen_val"]) <= 1e-12 * abs(case["eigen_val"]), name
+        assert np.max(np.abs(v - vecs[name])) <= 1e-12, name
+
+
+def test_residual_random_fp32(eigen):
+    # wrapper/python/test.py:3-18: DIM = 1024, 4 runs, A v ≈ λ v (atol 1e-3)
+    rng = np.random.default_rng(2021)
+    mat = rng.random((1024, 1024)).astype("f")
+    for _ in range(4):
+        lam, v, ts, itr = eigen.similarity_transform(mat)
+        assert np.all(np.isclose(mat @ v, lam * v, atol=1e-3)), "Av = λv assertion failed !"
+
+
+def test_deterministic(eigen, orc):
+    mat = orc.random_matrix(2000, 4)
+    a = eigen.similarity_transform(mat)
+    b = eigen.similarity_transform(mat)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1]) and a[3] == b[3]
+
+
+def test_input_not_modified(eigen, orc):
+    mat = orc.hilbert(300, np.float32)
+    keep = mat.copy()
+    eigen.similarity_transform(mat)
+    assert np.array_equal(mat, keep)       # similarity_transform.cpp:14,19
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+@pytest.mark.parametrize("n", [1, 2, 3, 5, 17, 63, 65, 257])
+def test_edge_sizes(eigen, orc, dt, n):
+    mat = orc.random_matrix(n, n, dt)
+    lam, v, ts, itr = eigen.similarity_transform(mat)
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL)
+    assert itr == ref.iter_count
+    tol = 1e-10 if dt == np.float64 else 1e-5
+    assert abs(lam - ref.eigen_val) <= tol * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= 10 * tol
+
+
+@pytest.mark.parametrize("dt", [np.float32, np.float64])
+def test_max_itr_exhaustion(eigen, orc, dt):
+    mat = orc.random_matrix(100, 3, dt)
+    lam, v, ts, itr, st = eigen.similarity_transform_ex(mat, eps=0.0, max_itr=5, batch=2)
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=5)
+    assert itr == ref.iter_count == 5 and st["converged"] == 0 and st["rounds"] == 5
+    tol = 1e-12 if dt == np.float64 else 1e-5
+    assert abs(lam - ref.eigen_val) <= tol * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= tol
+
+
+@pytest.mark.parametrize("batch", [1, 3, 8, 64])
+def test_batch_size_does_not_change_results(eigen, orc, batch):
+    mat = orc.hilbert(512)
+    base = eigen.similarity_transform(mat)
+    lam, v, ts, itr, st = eigen.similarity_transform_ex(mat, batch=batch, time_kernels=True)
+    assert lam == base[0] and np.array_equal(v, base[1]) and itr == base[3] == 12
+    assert st["fused_launches"] == itr and st["fused_ms_total"] > 0
+
+
+def test_device_solver(solver, orc):
+    a = dev.generate("hilbert", 2048, torch.float64, device=DEV)
+    keep = a.clone()
+    lam, v, itr, st = solver.solve(a)
+    assert torch.equal(a, keep)                               # not in place by default
+    ref = orc.similarity_transform(orc.hilbert(2048), orc.SEM_SYCL)
+    assert itr == ref.iter_count == 14
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(to_np(v) - ref.eigen_vec)) <= 1e-10
+    lam2, v2, itr2, _ = solver.solve(a, inplace=True)
+    assert lam2 == lam and torch.equal(v2, v)
+
+
+def test_large_random_vs_oracle(solver, orc):
+    n = 16384
+    a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    lam, v, itr, _ = solver.solve(a, inplace=True)
+    ref = orc.similarity_transform(orc.random_matrix(n, 0), orc.SEM_SYCL, nthreads=16)
+    assert itr == ref.iter_count
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(to_np(v) - ref.eigen_vec)) <= 1e-10
+
+
+def test_full_size_properties(solver):
+    # BASELINE config 3 size (32768^2 fp64 = 8 GiB): size-independent checks
+    n = 32768
+    a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    lam, v, itr, _ = solver.solve(a, inplace=True)
+    dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
+    r = torch.mv(a, v) - lam * v                       # torch fp64 as the checker only
+    assert (r.abs().max() / (lam * v.abs().max())).item() < 1e-9
+    # homogeneity: 2A has eigenvalue 2λ with the identical eigenvector, bit for bit
+    a.mul_(2.0)
+    lam2, v2, itr2, _ = solver.solve(a, inplace=True)
+    assert lam2 == 2.0 * lam and itr2 == itr and torch.equal(v2, v)
+    del a
+    torch.cuda.empty_cache()
+
+
+def test_cpp_kernel_tests():
+    # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run(["make", "-s", "-C", os.path.join(here, "cpp")], check=True)
+    out = subprocess.run([os.path.join(here, "cpp", "test_kernels")], capture_output=True,
+                         text=True, timeout=300)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "similarity transform worked" in out.stdout

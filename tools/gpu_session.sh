@@ -1,0 +1,45 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel trace.
+# Usage (through gpurun, from the repo root): bash tools/gpu_session.sh TAG [steps...]
+#   steps: tests smoke bench prof pmc tune (default: tests smoke bench prof)
+# Every GPU step has its own time limit; a crash/abort/timeout ends the
+# session (test assertion failures, exit 1, do not).
+set -u
+TAG=${1:-run}; shift || true
+STEPS=${*:-tests smoke bench prof}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+
+step() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 15 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+    echo "== stopping: $name exited $rc" | tee -a "$OUT/session.log"
+    exit $rc
+  fi
+  return $rc
+}
+
+rocm-smi --showproductname > "$OUT/device.txt" 2>&1 || true
+nproc > "$OUT/host.txt"; lscpu | grep -E 'Model name|^CPU\(s\)' >> "$OUT/host.txt" || true
+
+for s in $STEPS; do
+  case $s in
+    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -rA ;;
+    smoke) step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
+    bench) step bench 600 python bench.py ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu ;;
+    pmc)
+      step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
+      step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
+    tune)  step tune 600 ./tools/tune_fused ;;
+  esac
+done
+echo "== session done" | tee -a "$OUT/session.log"
