@@ -120,8 +120,8 @@ st(V* p, const V& v)
 // per chunk and reused for the ROWS rows.
 // ---------------------------------------------------------------------------
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER,
-          bool NT>
-__global__ __launch_bounds__(kBlock) void
+          bool NT, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
 k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
         uint32_t row_begin, uint32_t ncols, uint32_t row0,
         const st_state* __restrict__ state)
@@ -153,11 +153,11 @@ k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     for (int u = 0; u < UU; u++)
 #pragma unroll
       for (int j = 0; j < ROWS; j++)
-        x[u][j] = ld<V, NT>(rowp[j] + c + u * kBlock);
+        x[u][j] = ld<V, NT>(rowp[j] + c + u * BLK);
     if constexpr (SCALE) {
 #pragma unroll
       for (int u = 0; u < UU; u++)
-        sc[u] = sv[c + u * kBlock];
+        sc[u] = sv[c + u * BLK];
 #pragma unroll
       for (int u = 0; u < UU; u++)
 #pragma unroll
@@ -171,7 +171,7 @@ k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
       for (int u = 0; u < UU; u++)
 #pragma unroll
         for (int j = 0; j < ROWS; j++)
-          st<V, NT>(rowp[j] + c + u * kBlock, x[u][j]);
+          st<V, NT>(rowp[j] + c + u * BLK, x[u][j]);
     }
     if constexpr (SUM) {
 #pragma unroll
@@ -183,14 +183,14 @@ k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
   };
 
   uint32_t c = threadIdx.x;
-  for (; c + (U - 1) * kBlock < nv; c += U * kBlock)
+  for (; c + (U - 1) * BLK < nv; c += U * BLK)
     body(c, std::integral_constant<int, U>{});
   if constexpr (U > 1)
-    for (; c < nv; c += kBlock)
+    for (; c < nv; c += BLK)
       body(c, std::integral_constant<int, 1>{});
 
   if constexpr (SUM) {
-    __shared__ T red[kWaves][ROWS];
+    __shared__ T red[(BLK / 64)][ROWS];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
 #pragma unroll
@@ -203,7 +203,7 @@ k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     if (threadIdx.x < ROWS) {
       T t = red[0][threadIdx.x];
 #pragma unroll
-      for (int w = 1; w < kWaves; w++)
+      for (int w = 1; w < (BLK / 64); w++)
         t += red[w][threadIdx.x];
       s_next[rbase + threadIdx.x] = t;
     }
