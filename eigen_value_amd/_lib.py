@@ -110,6 +110,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.max_eigen_value_ex.restype = i64
     L.st_set_stream.argtypes = [P, P]
     L.st_set_stream.restype = i32
+    L.st_use_own_stream.argtypes = [P]
+    L.st_use_own_stream.restype = i32
     for sfx, T in (("f32", f32), ("f64", f64)):
         fn = getattr(L, f"st_solve_device_{sfx}")
         fn.argtypes = [P, P, u32, P, P, P, P, P, P]

@@ -112,100 +112,111 @@ st(V* p, const V& v)
 // ---------------------------------------------------------------------------
 // fused scale + row-sum  (plain row-sum when SCALE == false)
 //
-// Workgroup b owns the ROWS consecutive local rows
-// [row_begin + b*ROWS, +ROWS) (always full; the host launches the remainder
-// rows with ROWS = 1) and sweeps their full width, W elements (16 bytes) per
-// lane per access, U column chunks per iteration so that U*ROWS 16-byte
-// loads are in flight per lane.  The column scale s_cur[c] is loaded once
-// per chunk and reused for the ROWS rows.
+// A row group is ROWS consecutive local rows [row_begin + g*ROWS, +ROWS)
+// (always full; the host launches remainder rows with ROWS = 1).  Workgroup b
+// takes groups g = b, b + gridDim.x, ... (grid-stride: the host may cap the
+// grid below the group count), and sweeps each group's full width, W
+// elements (16 bytes) per lane per access, U column chunks per iteration so
+// that U*ROWS 16-byte loads are in flight per lane.  The column scale
+// s_cur[c] is loaded once per chunk and reused for the ROWS rows.
+//
+// a_out == a_in is the in-place transform of the reference
+// (similarity_transform.cpp:324); a_out != a_in writes A_{k+1} to a second
+// buffer (ping-pong layout).  NT selects non-temporal (streaming) loads and
+// stores for the matrix.
 // ---------------------------------------------------------------------------
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER,
           bool NT, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
-k_fused(T* __restrict__ a, const T* __restrict__ s_cur, T* __restrict__ s_next,
-        uint32_t row_begin, uint32_t ncols, uint32_t row0,
-        const st_state* __restrict__ state)
+k_fused(const T* a_in, T* a_out, const T* __restrict__ s_cur,
+        T* __restrict__ s_next, uint32_t row_begin, uint32_t ngroups,
+        uint32_t ncols, uint32_t row0, const st_state* __restrict__ state)
 {
   using V = typename vec<T, W>::type;
   if (state != nullptr && state->done)
     return;
 
-  const uint32_t rbase = row_begin + blockIdx.x * ROWS;
   const uint32_t nv = ncols / W;
-
-  V* rowp[ROWS];
-  T inv[ROWS];
-  T acc[ROWS];
-#pragma unroll
-  for (int j = 0; j < ROWS; j++) {
-    rowp[j] = reinterpret_cast<V*>(a + (size_t)(rbase + j) * ncols);
-    if constexpr (SCALE)
-      inv[j] = (T)1 / s_cur[row0 + rbase + j];
-    acc[j] = (T)0;
-  }
   const V* sv = reinterpret_cast<const V*>(s_cur);
+  __shared__ T red[BLK / 64][ROWS];
 
-  auto body = [&](uint32_t c, auto ucount) {
-    constexpr int UU = decltype(ucount)::value;
-    V x[UU][ROWS];
-    V sc[UU];
-#pragma unroll
-    for (int u = 0; u < UU; u++)
-#pragma unroll
-      for (int j = 0; j < ROWS; j++)
-        x[u][j] = ld<V, NT>(rowp[j] + c + u * BLK);
-    if constexpr (SCALE) {
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-        sc[u] = sv[c + u * BLK];
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < ROWS; j++) {
-          if constexpr (ORDER == 0)
-            x[u][j] = x[u][j] * (inv[j] * sc[u]); // sim_transform.cpp:324-325
-          else
-            x[u][j] = (inv[j] * x[u][j]) * sc[u]; // main.py:13-16
-        }
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < ROWS; j++)
-          st<V, NT>(rowp[j] + c + u * BLK, x[u][j]);
-    }
-    if constexpr (SUM) {
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < ROWS; j++)
-          acc[j] += hsum<T, W>(x[u][j]);
-    }
-  };
-
-  uint32_t c = threadIdx.x;
-  for (; c + (U - 1) * BLK < nv; c += U * BLK)
-    body(c, std::integral_constant<int, U>{});
-  if constexpr (U > 1)
-    for (; c < nv; c += BLK)
-      body(c, std::integral_constant<int, 1>{});
-
-  if constexpr (SUM) {
-    __shared__ T red[(BLK / 64)][ROWS];
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint32_t rbase = row_begin + g * ROWS;
+    const V* rin[ROWS];
+    V* rout[ROWS];
+    T inv[ROWS];
+    T acc[ROWS];
 #pragma unroll
     for (int j = 0; j < ROWS; j++) {
-      T t = wave_sum(acc[j]);
-      if (lane == 0)
-        red[wave][j] = t;
+      rin[j] = reinterpret_cast<const V*>(a_in + (size_t)(rbase + j) * ncols);
+      rout[j] = reinterpret_cast<V*>(a_out + (size_t)(rbase + j) * ncols);
+      if constexpr (SCALE)
+        inv[j] = (T)1 / s_cur[row0 + rbase + j];
+      acc[j] = (T)0;
     }
-    __syncthreads();
-    if (threadIdx.x < ROWS) {
-      T t = red[0][threadIdx.x];
+
+    auto body = [&](uint32_t c, auto ucount) {
+      constexpr int UU = decltype(ucount)::value;
+      V x[UU][ROWS];
+      V sc[UU];
 #pragma unroll
-      for (int w = 1; w < (BLK / 64); w++)
-        t += red[w][threadIdx.x];
-      s_next[rbase + threadIdx.x] = t;
+      for (int u = 0; u < UU; u++)
+#pragma unroll
+        for (int j = 0; j < ROWS; j++)
+          x[u][j] = ld<V, NT>(rin[j] + c + u * BLK);
+      if constexpr (SCALE) {
+#pragma unroll
+        for (int u = 0; u < UU; u++)
+          sc[u] = sv[c + u * BLK];
+#pragma unroll
+        for (int u = 0; u < UU; u++)
+#pragma unroll
+          for (int j = 0; j < ROWS; j++) {
+            if constexpr (ORDER == 0)
+              x[u][j] = x[u][j] * (inv[j] * sc[u]); // sim_transform.cpp:324-325
+            else
+              x[u][j] = (inv[j] * x[u][j]) * sc[u]; // main.py:13-16
+          }
+#pragma unroll
+        for (int u = 0; u < UU; u++)
+#pragma unroll
+          for (int j = 0; j < ROWS; j++)
+            st<V, NT>(rout[j] + c + u * BLK, x[u][j]);
+      }
+      if constexpr (SUM) {
+#pragma unroll
+        for (int u = 0; u < UU; u++)
+#pragma unroll
+          for (int j = 0; j < ROWS; j++)
+            acc[j] += hsum<T, W>(x[u][j]);
+      }
+    };
+
+    uint32_t c = threadIdx.x;
+    for (; c + (U - 1) * BLK < nv; c += U * BLK)
+      body(c, std::integral_constant<int, U>{});
+    if constexpr (U > 1)
+      for (; c < nv; c += BLK)
+        body(c, std::integral_constant<int, 1>{});
+
+    if constexpr (SUM) {
+      const int lane = threadIdx.x & 63;
+      const int wave = threadIdx.x >> 6;
+#pragma unroll
+      for (int j = 0; j < ROWS; j++) {
+        T t = wave_sum(acc[j]);
+        if (lane == 0)
+          red[wave][j] = t;
+      }
+      __syncthreads();
+      if (threadIdx.x < ROWS) {
+        T t = red[0][threadIdx.x];
+#pragma unroll
+        for (int w = 1; w < BLK / 64; w++)
+          t += red[w][threadIdx.x];
+        s_next[rbase + threadIdx.x] = t;
+      }
+      __syncthreads(); // red[] is reused by the next group
     }
   }
 }

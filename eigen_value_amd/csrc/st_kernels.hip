@@ -54,8 +54,8 @@ launch_cfg(T* a, const T* s_cur, T* s_next, uint32_t row_begin,
     return;
   hipLaunchKernelGGL(
     (dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, kNontemporal>),
-    dim3(nblocks), dim3(kBlock), 0, stream, a, s_cur, s_next, row_begin, ncols,
-    row0, st);
+    dim3(nblocks), dim3(kBlock), 0, stream, a, a, s_cur, s_next, row_begin,
+    nblocks, ncols, row0, st);
 }
 
 template <typename T, int W, bool SCALE, bool SUM, int ORDER>

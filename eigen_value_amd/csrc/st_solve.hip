@@ -418,7 +418,19 @@ st_set_stream(void* wq, void* stream)
   st::clear_error();
   Context* c = st::as_ctx(wq);
   ST_REQUIRE(c, "st_set_stream: null queue");
-  c->stream = stream ? reinterpret_cast<hipStream_t>(stream) : c->own_stream;
+  // NULL is HIP's null stream (torch's default stream handle is 0), not
+  // "no stream": the context must order itself after the caller's work
+  c->stream = reinterpret_cast<hipStream_t>(stream);
+  return 0;
+}
+
+int
+st_use_own_stream(void* wq)
+{
+  st::clear_error();
+  Context* c = st::as_ctx(wq);
+  ST_REQUIRE(c, "st_use_own_stream: null queue");
+  c->stream = c->own_stream;
   return 0;
 }
 

@@ -109,9 +109,12 @@ int64_t max_eigen_value_ex(void* wq, int dtype, const void* mat,
                            unsigned int dim, unsigned int* iter_cnt,
                            const st_options* opt, st_stats* stats);
 
-/* Make the context launch on a caller stream (hipStream_t; NULL restores
- * the context's own stream).  Returns 0 or negative. */
+/* Make the context launch on a caller stream (a hipStream_t; NULL is the
+ * HIP null stream, which is torch's default stream).  Returns 0 or
+ * negative.  st_use_own_stream restores the context's own non-blocking
+ * stream (the make_queue default). */
 int st_set_stream(void* wq, void* stream);
+int st_use_own_stream(void* wq);
 
 /* ---------------------------------------------------------------------- */
 /* 3. device-resident solve                                                */

@@ -277,10 +277,16 @@ def test_full_size_properties(solver):
     dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
     r = torch.mv(a, v) - lam * v                       # torch fp64 as the checker only
     assert (r.abs().max() / (lam * v.abs().max())).item() < 1e-9
-    # homogeneity: 2A has eigenvalue 2λ with the identical eigenvector, bit for bit
+    # homogeneity over a fixed number of rounds: every quantity of the
+    # iteration on 2A is exactly twice (s, λ) or equal to (v, D^-1 A D
+    # ratios) that on A, bit for bit
+    dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
+    lam4, v4, it4, _ = solver.solve(a, eps=0.0, max_itr=4, inplace=True)
+    dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
     a.mul_(2.0)
-    lam2, v2, itr2, _ = solver.solve(a, inplace=True)
-    assert lam2 == 2.0 * lam and itr2 == itr and torch.equal(v2, v)
+    lam8, v8, it8, _ = solver.solve(a, eps=0.0, max_itr=4, inplace=True)
+    assert it4 == it8 == 4
+    assert lam8 == 2.0 * lam4 and torch.equal(v8, v4)
     del a
     torch.cuda.empty_cache()
 

@@ -48,6 +48,25 @@ k_stream_rw(d2* __restrict__ a, size_t n2, double f)
   }
 }
 
+template <bool NT>
+__global__ __launch_bounds__(256) void
+k_stream_copy(const d2* __restrict__ a, d2* __restrict__ b, size_t n2, double f)
+{
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n2;
+       i += (size_t)gridDim.x * 256) {
+    d2 x;
+    if constexpr (NT)
+      x = __builtin_nontemporal_load(a + i);
+    else
+      x = a[i];
+    x *= f;
+    if constexpr (NT)
+      __builtin_nontemporal_store(x, b + i);
+    else
+      b[i] = x;
+  }
+}
+
 // ceiling reference 2: streaming read-only sum
 __global__ __launch_bounds__(256) void
 k_stream_r(const d2* __restrict__ a, size_t n2, double* out)
@@ -91,40 +110,44 @@ struct Timer
 };
 
 static double* g_a;
+static double* g_b;
 static double* g_s;
 static double* g_sn;
 static unsigned g_n;
 
 template <int ROWS, int U, bool NT, int BLK>
 void
-fused_variant(Timer& tm, int reps)
+fused_variant(Timer& tm, int reps, unsigned grid_cap = 0, bool oop = false)
 {
-  const unsigned nb = g_n / ROWS;
+  const unsigned ng = g_n / ROWS;
+  const unsigned grid = grid_cap && grid_cap < ng ? grid_cap : ng;
+  double* out = oop ? g_b : g_a;
   auto f = [&] {
     hipLaunchKernelGGL((k_fused<double, ROWS, 2, U, true, true, 0, NT, BLK>),
-                       dim3(nb), dim3(BLK), 0, 0, g_a, g_s, g_sn, 0u, g_n, 0u,
-                       nullptr);
+                       dim3(grid), dim3(BLK), 0, 0, g_a, out, g_s, g_sn, 0u, ng,
+                       g_n, 0u, nullptr);
   };
   float ms = tm.run(f, reps);
   double gb = 2.0 * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
-  std::printf("fused  rows=%d u=%d nt=%d blk=%4d  %8.4f ms  %7.1f GB/s\n",
-              ROWS, U, (int)NT, BLK, ms, gb);
+  std::printf("fused  rows=%d u=%d nt=%d blk=%4d grid=%6u oop=%d  %8.4f ms  %7.1f GB/s\n",
+              ROWS, U, (int)NT, BLK, grid, (int)oop, ms, gb);
 }
 
 template <int ROWS, int U, int BLK>
 void
-rowsum_variant(Timer& tm, int reps)
+rowsum_variant(Timer& tm, int reps, unsigned grid_cap = 0)
 {
-  const unsigned nb = g_n / ROWS;
+  const unsigned ng = g_n / ROWS;
+  const unsigned grid = grid_cap && grid_cap < ng ? grid_cap : ng;
   auto f = [&] {
     hipLaunchKernelGGL((k_fused<double, ROWS, 2, U, false, true, 0, false, BLK>),
-                       dim3(nb), dim3(BLK), 0, 0, g_a, nullptr, g_sn, 0u, g_n,
-                       0u, nullptr);
+                       dim3(grid), dim3(BLK), 0, 0, g_a, g_a, nullptr, g_sn, 0u,
+                       ng, g_n, 0u, nullptr);
   };
   float ms = tm.run(f, reps);
   double gb = 1.0 * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
-  std::printf("rowsum rows=%d u=%d blk=%4d        %8.4f ms  %7.1f GB/s\n", ROWS,
-              U, BLK, ms, gb);
+  std::printf("rowsum rows=%d u=%d blk=%4d grid=%6u        %8.4f ms  %7.1f GB/s\n",
+              ROWS, U, BLK, grid, ms, gb);
 }
 
 int
@@ -134,6 +157,7 @@ main(int argc, char** argv)
   const int reps = argc > 2 ? std::atoi(argv[2]) : 20;
   const size_t nn = (size_t)g_n * g_n;
   HIPCHECK(hipMalloc(&g_a, nn * 8));
+  HIPCHECK(hipMalloc(&g_b, nn * 8));
   HIPCHECK(hipMalloc(&g_s, (size_t)g_n * 8));
   HIPCHECK(hipMalloc(&g_sn, (size_t)g_n * 8));
   hipLaunchKernelGGL((k_generate<double, kRandom>), dim3(65536), dim3(256), 0,
@@ -167,30 +191,48 @@ main(int argc, char** argv)
     std::printf("stream_r  grid=%5u          %8.4f ms  %7.1f GB/s\n", grid, ms,
                 1.0 * nn * 8 / (ms * 1e-3) / 1e9);
   }
-  fused_variant<1, 1, false, 256>(tm, reps);
-  fused_variant<1, 2, false, 256>(tm, reps);
-  fused_variant<1, 4, false, 256>(tm, reps);
-  fused_variant<2, 1, false, 256>(tm, reps);
-  fused_variant<2, 2, false, 256>(tm, reps);
-  fused_variant<2, 4, false, 256>(tm, reps);
-  fused_variant<4, 1, false, 256>(tm, reps);
+  for (unsigned grid : { 1024u, 2048u }) {
+    auto f = [&] {
+      hipLaunchKernelGGL(k_stream_copy<false>, dim3(grid), dim3(256), 0, 0,
+                         (const d2*)g_a, (d2*)g_b, nn / 2, 1.0);
+    };
+    float ms = tm.run(f, reps);
+    std::printf("stream_copy grid=%5u        %8.4f ms  %7.1f GB/s\n", grid, ms,
+                2.0 * nn * 8 / (ms * 1e-3) / 1e9);
+    auto g = [&] {
+      hipLaunchKernelGGL(k_stream_copy<true>, dim3(grid), dim3(256), 0, 0,
+                         (const d2*)g_a, (d2*)g_b, nn / 2, 1.0);
+    };
+    ms = tm.run(g, reps);
+    std::printf("stream_copy_nt grid=%5u     %8.4f ms  %7.1f GB/s\n", grid, ms,
+                2.0 * nn * 8 / (ms * 1e-3) / 1e9);
+  }
+  // full grid (one group per workgroup)
   fused_variant<4, 2, false, 256>(tm, reps);
-  fused_variant<4, 4, false, 256>(tm, reps);
-  fused_variant<8, 1, false, 256>(tm, reps);
-  fused_variant<8, 2, false, 256>(tm, reps);
-  fused_variant<4, 2, true, 256>(tm, reps);
   fused_variant<2, 2, true, 256>(tm, reps);
   fused_variant<1, 4, true, 256>(tm, reps);
-  fused_variant<1, 2, false, 512>(tm, reps);
-  fused_variant<2, 2, false, 512>(tm, reps);
-  fused_variant<1, 2, false, 1024>(tm, reps);
-  fused_variant<1, 1, false, 1024>(tm, reps);
-  fused_variant<2, 1, false, 512>(tm, reps);
+  fused_variant<2, 4, true, 256>(tm, reps);
+  fused_variant<4, 2, true, 256>(tm, reps);
+  // capped grids (grid-stride over row groups)
+  for (unsigned cap : { 512u, 1024u, 2048u }) {
+    fused_variant<1, 4, true, 256>(tm, reps, cap);
+    fused_variant<2, 2, true, 256>(tm, reps, cap);
+    fused_variant<2, 4, true, 256>(tm, reps, cap);
+    fused_variant<4, 2, true, 256>(tm, reps, cap);
+    fused_variant<2, 2, false, 256>(tm, reps, cap);
+    fused_variant<1, 4, true, 512>(tm, reps, cap);
+  }
+  // out of place (ping-pong)
+  fused_variant<2, 2, true, 256>(tm, reps, 0, true);
+  fused_variant<2, 2, true, 256>(tm, reps, 1024, true);
+  fused_variant<1, 4, true, 256>(tm, reps, 1024, true);
+  fused_variant<2, 2, false, 256>(tm, reps, 1024, true);
   rowsum_variant<1, 2, 256>(tm, reps);
-  rowsum_variant<4, 2, 256>(tm, reps);
-  rowsum_variant<4, 4, 256>(tm, reps);
   rowsum_variant<2, 4, 512>(tm, reps);
+  rowsum_variant<2, 4, 256>(tm, reps, 1024);
+  rowsum_variant<1, 4, 256>(tm, reps, 1024);
   HIPCHECK(hipFree(g_a));
+  HIPCHECK(hipFree(g_b));
   HIPCHECK(hipFree(g_s));
   HIPCHECK(hipFree(g_sn));
   return 0;
