@@ -6,9 +6,10 @@
                     [--no-north-star]
 
 One *step* = one round of the hot path on the HBM-resident matrix: the
-O(N) epilogue (max, eigenvector update, stop test) plus the fused
-scale+row-sum kernel that moves 2*N^2*b bytes (read A_k, write A_{k+1}),
-plus, for N > 1 GPUs, the all-gather of the row-sum vector.  The stop
+single fused launch (max / eigenvector update / stop test of s_k, then
+A_{k+1} = D^-1 A_k D in place and its row sums) that moves 2*N^2*b bytes
+(read A_k, write A_{k+1}), plus, for N > 1 GPUs, the all-gather of the
+row-sum vector.  The stop
 tolerance is set to 0 inside the timed region so that every one of the K
 rounds does the full work (after convergence the reference would stop;
 a fixed round count is how SURVEY.md §8d prices ms/iteration).
@@ -91,17 +92,16 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    p, cur = sh.part, None
+    p = sh.part
     for k in range(steps):
         cur = sh.cur
-        s_k = sh.s[cur][:p.n]
-        sh.ops.epilogue(s_k, sh.v, sh.state, 0.0, 2**31, sh.semantics)
         ev[k][0].record()
-        sh.ops.scale_rowsum(sh.mat, s_k, sh._slot(sh.s[cur ^ 1])[:p.nrows], p.row0,
-                            sh.semantics, sh.state)
+        sh.ops.round(sh.mat, sh.s[cur][:p.n], sh._slot(sh.s[cur ^ 1]), sh.v, p.row0,
+                     0.0, sh.k, 2**31, sh.semantics, sh.state)
         ev[k][1].record()
         sh.gather(sh.s[cur ^ 1])
         sh.cur = cur ^ 1
+        sh.k += 1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -167,7 +167,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic[0],
-                "kernel": "k_fused (scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
+                "kernel": "k_round (fused stats + scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
                 "traffic_source": None if traffic is None else traffic[1]}
 

@@ -58,7 +58,9 @@ class st_state(ctypes.Structure):
                 ("stop", ctypes.c_uint32),
                 ("lambda_", ctypes.c_double),
                 ("max", ctypes.c_double),
-                ("pad", ctypes.c_uint64 * 4)]
+                ("end", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32),
+                ("pad", ctypes.c_uint64 * 3)]
 
 
 assert ctypes.sizeof(st_state) == 64
@@ -123,8 +125,10 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"st_rowsum_{sfx}").argtypes = [P, P, u32, u32, P]
         getattr(L, f"st_scale_rowsum_{sfx}").argtypes = [P, P, P, u32, u32, u32, u32, P, P]
         getattr(L, f"st_epilogue_{sfx}").argtypes = [P, P, u32, T, u32, u32, P, P]
+        getattr(L, f"st_round_{sfx}").argtypes = [P, P, P, P, u32, u32, u32, T, u32, u32,
+                                                  u32, P, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
-                     "fill", "rowsum", "scale_rowsum", "epilogue"):
+                     "fill", "rowsum", "scale_rowsum", "epilogue", "round"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32

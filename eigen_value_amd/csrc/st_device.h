@@ -222,6 +222,217 @@ k_fused(const T* a_in, T* a_out, const T* __restrict__ s_cur,
 }
 
 // ---------------------------------------------------------------------------
+// one whole round in one launch (the solve loop's kernel)
+//
+// Round k of similarity_transform.cpp:39-53 for the local rows, given the
+// FULL row-sum vector s_k (s_cur, length ncols) that the previous launch
+// produced:
+//   m_k    = max(0, max s_k)                       find_max        (cpp:154)
+//   v[r]  *= s_k[r] / m_k   for the local rows     compute_eigen_v (cpp:260)
+//   stop_k = all |s_k[i] - s_k[i+1]| < eps         stop            (cpp:413)
+//   A     <- D_k^-1 A D_k, s_{k+1} = rowsum(A)     compute_next + sum_across
+// Every workgroup reads all of s_k anyway (column scales), so each one
+// derives m_k and stop_k redundantly from its first row group's sweep
+// (max and a boolean AND are order-independent: every workgroup, and every
+// rank of a sharded solve, gets the identical answer); workgroup 0 records
+// the round in `state`.  There is no separate epilogue launch.
+//
+// After the stop round the reference performs no more transforms; here the
+// stop round's launch still writes A_{k+1}/s_{k+1} (never observable: the
+// matrix is the solver's private copy, cpp:14,19) and every later launch
+// returns at once: state->end = k+1 is set by the stop round, and launch j
+// exits if end != 0 && end <= j (a launch never gates on its own round).
+// ---------------------------------------------------------------------------
+template <typename T, int R, int W, int U, int ORDER, bool NT, int BLK,
+          bool STATS>
+__device__ __forceinline__ void
+round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+            uint32_t rbase, uint32_t ncols, uint32_t row0, bool cyclic, T eps,
+            T& mx, int& ok, T (*red)[4])
+{
+  using V = typename vec<T, W>::type;
+  const uint32_t nv = ncols / W;
+  const V* sv = reinterpret_cast<const V*>(s_cur);
+  V* rows[R];
+  T inv[R];
+  T acc[R];
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    rows[j] = reinterpret_cast<V*>(a + (size_t)(rbase + j) * ncols);
+    inv[j] = (T)1 / s_cur[row0 + rbase + j];
+    acc[j] = (T)0;
+  }
+  auto body = [&](uint32_t c, auto ucount) {
+    constexpr int UU = decltype(ucount)::value;
+    V x[UU][R];
+    V sc[UU];
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        x[u][j] = ld<V, NT>(rows[j] + c + u * BLK);
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+      sc[u] = sv[c + u * BLK];
+    if constexpr (STATS) {
+#pragma unroll
+      for (int u = 0; u < UU; u++) {
+        const uint32_t q = c + u * BLK; // vector index: columns q*W ..
+        T e[W + 1];
+        if constexpr (W == 1) {
+          e[0] = sc[u];
+        } else {
+#pragma unroll
+          for (int i = 0; i < W; i++)
+            e[i] = sc[u][i];
+        }
+        const uint32_t nxt = (q + 1) * W;
+        const bool has_next = nxt < ncols || cyclic;
+        e[W] = s_cur[nxt < ncols ? nxt : 0];
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          mx = e[i] > mx ? e[i] : mx;
+          if (i < W - 1 || has_next) {
+            const T d = e[i] - e[i + 1];
+            ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0; // cpp:419-421
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        if constexpr (ORDER == 0)
+          x[u][j] = x[u][j] * (inv[j] * sc[u]); // cpp:324-325
+        else
+          x[u][j] = (inv[j] * x[u][j]) * sc[u]; // main.py:13-16
+      }
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        st<V, NT>(rows[j] + c + u * BLK, x[u][j]);
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        acc[j] += hsum<T, W>(x[u][j]);
+  };
+  uint32_t c = threadIdx.x;
+  for (; c + (U - 1) * BLK < nv; c += U * BLK)
+    body(c, std::integral_constant<int, U>{});
+  if constexpr (U > 1)
+    for (; c < nv; c += BLK)
+      body(c, std::integral_constant<int, 1>{});
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    T t = wave_sum(acc[j]);
+    if (lane == 0)
+      red[wave][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    T t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < BLK / 64; w++)
+      t += red[w][threadIdx.x];
+    s_next[rbase + threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+template <typename T, int ROWS, int W, int U, int ORDER, bool NT,
+          int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+        T* __restrict__ v, uint32_t ng_main, uint32_t nrem, uint32_t ncols,
+        uint32_t row0, T eps, uint32_t k, uint32_t max_itr,
+        uint32_t semantics, st_state* state)
+{
+  static_assert(ROWS <= 4, "red[] holds 4 rows");
+  {
+    const uint32_t e =
+      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0 && e <= k)
+      return; // a previous round stopped
+  }
+  __shared__ T red[BLK / 64][4];
+  __shared__ T mx_sh[BLK / 64];
+  __shared__ T m_sh;
+  const bool cyclic = semantics == ST_SEM_SYCL;
+  const uint32_t ngroups = ng_main + nrem;
+  T mx = (T)0; // find_max starts from 0 (cpp:185)
+  int ok = 1;
+  T dummy_mx = 0;
+  int dummy_ok = 1;
+
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const bool first = g == blockIdx.x;
+    if (g < ng_main) {
+      if (first)
+        round_group<T, ROWS, W, U, ORDER, NT, BLK, true>(
+          a, s_cur, s_next, g * ROWS, ncols, row0, cyclic, eps, mx, ok, red);
+      else
+        round_group<T, ROWS, W, U, ORDER, NT, BLK, false>(
+          a, s_cur, s_next, g * ROWS, ncols, row0, cyclic, eps, dummy_mx,
+          dummy_ok, red);
+    } else {
+      const uint32_t rb = ng_main * ROWS + (g - ng_main);
+      if (first)
+        round_group<T, 1, W, U, ORDER, NT, BLK, true>(
+          a, s_cur, s_next, rb, ncols, row0, cyclic, eps, mx, ok, red);
+      else
+        round_group<T, 1, W, U, ORDER, NT, BLK, false>(
+          a, s_cur, s_next, rb, ncols, row0, cyclic, eps, dummy_mx, dummy_ok,
+          red);
+    }
+  }
+
+  // m_k and stop_k over the whole vector (this workgroup's copy)
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0)
+    mx_sh[threadIdx.x >> 6] = mx;
+  const int stop = __syncthreads_and(ok);
+  if (threadIdx.x == 0) {
+    T m = mx_sh[0];
+#pragma unroll
+    for (int w = 1; w < BLK / 64; w++)
+      m = mx_sh[w] > m ? mx_sh[w] : m;
+    m_sh = m;
+  }
+  __syncthreads();
+  const T m = m_sh;
+  // v[r] *= s_k[r] / m_k for this workgroup's rows (cpp:260)
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const uint32_t rb = g < ng_main ? g * ROWS : ng_main * ROWS + (g - ng_main);
+    const uint32_t nr = g < ng_main ? ROWS : 1;
+    if (threadIdx.x < nr) {
+      const uint32_t r = row0 + rb + threadIdx.x;
+      v[r] = v[r] * (s_cur[r] / m);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    state->lambda = (double)s_cur[0]; // cpp:60-65
+    state->max = (double)m;
+    state->stop = stop ? 1u : 0u;
+    state->round = k;
+    if (stop) {
+      state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
+      state->end = k + 1;
+      state->done = 1u;
+    } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
+      state->iters = max_itr;
+      state->end = k + 1;
+      state->done = 1u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // round epilogue: one workgroup over the full row-sum vector
 // ---------------------------------------------------------------------------
 template <typename T>

@@ -38,11 +38,14 @@ check_launch(const char* what)
   return 0;
 }
 
-// Tuned shape of the fused stream (see tools/tune_fused.hip and
-// profiles/): rows per workgroup and column chunks in flight per lane.
-constexpr int kRows = 4;
-constexpr int kUnroll = 2;
-constexpr bool kNontemporal = false;
+// Tuned shape of the fused stream (tools/tune_fused.hip, tools/stream_bench
+// .hip; profiles/r01_tuning.md): 2 rows per group, 4 column chunks of 16 B
+// in flight per lane per row, non-temporal matrix loads/stores, at most
+// kGridCap workgroups (2 per CU) striding over the row groups.
+constexpr int kRows = 2;
+constexpr int kUnroll = 4;
+constexpr bool kNontemporal = true;
+constexpr uint32_t kGridCap = 512;
 
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER>
 void
@@ -52,9 +55,10 @@ launch_cfg(T* a, const T* s_cur, T* s_next, uint32_t row_begin,
 {
   if (nblocks == 0)
     return;
+  const uint32_t grid = nblocks < kGridCap ? nblocks : kGridCap;
   hipLaunchKernelGGL(
     (dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, kNontemporal>),
-    dim3(nblocks), dim3(kBlock), 0, stream, a, a, s_cur, s_next, row_begin,
+    dim3(grid), dim3(kBlock), 0, stream, a, a, s_cur, s_next, row_begin,
     nblocks, ncols, row0, st);
 }
 
@@ -64,7 +68,7 @@ launch_rows(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
             uint32_t row0, const st_state* st, hipStream_t stream)
 {
   // small matrices: one row per workgroup keeps >= 256 workgroups busy
-  if (nrows < 2048) {
+  if (nrows < 2 * kGridCap) {
     launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(a, s_cur, s_next, 0, nrows,
                                                     ncols, row0, st, stream);
     return;
@@ -93,7 +97,75 @@ launch_vec(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
                                          st, stream);
 }
 
+template <typename T, int ROWS, int W, int ORDER>
+void
+launch_round_cfg(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
+                 uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+                 uint32_t max_itr, uint32_t semantics, st_state* st,
+                 hipStream_t stream)
+{
+  const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
+  const uint32_t ng = ng_main + nrem;
+  const uint32_t grid = ng < kGridCap ? ng : kGridCap;
+  hipLaunchKernelGGL((dev::k_round<T, ROWS, W, kUnroll, ORDER, kNontemporal>),
+                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, s_next, v,
+                     ng_main, nrem, ncols, row0, eps, k, max_itr, semantics,
+                     st);
+}
+
+template <typename T, int W, int ORDER>
+void
+launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
+                  uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+                  uint32_t max_itr, uint32_t semantics, st_state* st,
+                  hipStream_t stream)
+{
+  if (nrows < 2 * kGridCap)
+    launch_round_cfg<T, 1, W, ORDER>(a, s_cur, s_next, v, nrows, ncols, row0,
+                                     eps, k, max_itr, semantics, st, stream);
+  else
+    launch_round_cfg<T, kRows, W, ORDER>(a, s_cur, s_next, v, nrows, ncols,
+                                         row0, eps, k, max_itr, semantics, st,
+                                         stream);
+}
+
 } // namespace
+
+template <typename T>
+int
+launch_round(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
+             uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+             uint32_t max_itr, uint32_t semantics, st_state* st,
+             hipStream_t stream)
+{
+  ST_REQUIRE(s_cur && v && st, "round: null pointer");
+  ST_REQUIRE(a && s_next, "round: null pointer");
+  ST_REQUIRE(ncols > 0, "round: ncols must be > 0");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "round: bad semantics %u", semantics);
+  ST_REQUIRE(max_itr > 0, "round: max_itr must be > 0");
+  // every launch must own >= 1 row: the stop test and m_k are derived from
+  // the sweep of a row group (the sharded driver rejects empty row blocks)
+  ST_REQUIRE(nrows > 0, "round: nrows must be > 0");
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && aligned16(a) && aligned16(s_cur);
+  const bool order1 = semantics == ST_SEM_MAINPY;
+  if (vec_ok) {
+    if (order1)
+      launch_round_rows<T, W, 1>(a, s_cur, s_next, v, nrows, ncols, row0, eps,
+                                 k, max_itr, semantics, st, stream);
+    else
+      launch_round_rows<T, W, 0>(a, s_cur, s_next, v, nrows, ncols, row0, eps,
+                                 k, max_itr, semantics, st, stream);
+  } else {
+    if (order1)
+      launch_round_rows<T, 1, 1>(a, s_cur, s_next, v, nrows, ncols, row0, eps,
+                                 k, max_itr, semantics, st, stream);
+    else
+      launch_round_rows<T, 1, 0>(a, s_cur, s_next, v, nrows, ncols, row0, eps,
+                                 k, max_itr, semantics, st, stream);
+  }
+  return check_launch("round");
+}
 
 template <typename T>
 int
@@ -199,6 +271,13 @@ template int launch_epilogue<float>(const float*, float*, uint32_t, float,
 template int launch_epilogue<double>(const double*, double*, uint32_t, double,
                                      uint32_t, uint32_t, st_state*,
                                      hipStream_t);
+template int launch_round<float>(float*, const float*, float*, float*,
+                                 uint32_t, uint32_t, uint32_t, float, uint32_t,
+                                 uint32_t, uint32_t, st_state*, hipStream_t);
+template int launch_round<double>(double*, const double*, double*, double*,
+                                  uint32_t, uint32_t, uint32_t, double,
+                                  uint32_t, uint32_t, uint32_t, st_state*,
+                                  hipStream_t);
 template int launch_fill<float>(float*, uint64_t, float, hipStream_t);
 template int launch_fill<double>(double*, uint64_t, double, hipStream_t);
 
@@ -266,6 +345,17 @@ st_state_reset(st_state* d_state, void* stream)
     return st::launch_scale_rowsum<T>(d_mat, d_s_cur, d_s_next, nrows, ncols,  \
                                       row0, semantics, d_state,                \
                                       ST_STREAM(stream));                      \
+  }                                                                            \
+  int st_round_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next, T* d_v,          \
+                     unsigned int nrows, unsigned int ncols,                   \
+                     unsigned int row0, T eps, unsigned int k,                 \
+                     unsigned int max_itr, unsigned int semantics,             \
+                     st_state* d_state, void* stream)                          \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_round<T>(d_mat, d_s_cur, d_s_next, d_v, nrows, ncols,    \
+                               row0, eps, k, max_itr, semantics, d_state,      \
+                               ST_STREAM(stream));                             \
   }                                                                            \
   int st_epilogue_##SFX(const T* d_s, T* d_v, unsigned int n, T eps,           \
                         unsigned int max_itr, unsigned int semantics,          \

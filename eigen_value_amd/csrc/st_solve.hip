@@ -7,10 +7,11 @@
 //
 // Round loop (one device stream, no per-round host sync):
 //   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
-//   per round k:
-//     K2  epilogue(s_k): max, v *= s/m, stop test, lambda = s_k[0]
-//     K1  A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})
-//         (skipped on device once K2 has set done)
+//   per round k, ONE launch (k_round, st_device.h):
+//     from s_k: max, v *= s/m, stop test, lambda = s_k[0] (every workgroup
+//     derives m_k/stop_k from its own sweep of s_k; workgroup 0 records)
+//     A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})
+//     (launches after the stop round return at once)
 // The reference blocks on a host_accessor every round
 // (similarity_transform.cpp:45-50).  Here rounds are enqueued in batches;
 // the host checks the device `done` flag of batch b while batch b+1 is
@@ -210,9 +211,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   while (!done && enqueued < o.max_itr) {
     const uint32_t b = (o.max_itr - enqueued) < o.batch ? (o.max_itr - enqueued)
                                                         : o.batch;
-    for (uint32_t k = 0; k < b; k++) {
-      rc |= launch_epilogue<T>(s_buf[cur], d_v, n, eps, o.max_itr, o.semantics,
-                               c->d_state, s);
+    for (uint32_t j = 0; j < b; j++) {
+      const uint32_t k = enqueued + j;
       hipEvent_t ea = nullptr, eb = nullptr;
       if (timed) {
         rc |= mk(&ea) | mk(&eb);
@@ -220,8 +220,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
         ev.push_back(eb);
         (void)hipEventRecord(ea, s);
       }
-      rc |= launch_scale_rowsum<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], n, n, 0,
-                                   o.semantics, c->d_state, s);
+      rc |= launch_round<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_v, n, n, 0,
+                            eps, k, o.max_itr, o.semantics, c->d_state, s);
       if (timed)
         (void)hipEventRecord(eb, s);
       cur ^= 1;
@@ -260,16 +260,15 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     std::memset(stats, 0, sizeof(*stats));
     stats->loop_ms = loop_ms;
     stats->d2h_ms = d2h_ms;
-    stats->rounds = fin.stop ? fin.round + 1 : fin.round;
+    stats->rounds = fin.end;
     stats->converged = fin.stop;
     if (timed) {
       float ms = 0.f;
       (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
       stats->rowsum_ms = ms;
-      // transforms actually executed: rounds that did not stop, minus the
-      // device-skipped one at max_itr
-      uint32_t transforms = fin.stop ? fin.round
-                                     : (fin.round > 0 ? fin.round - 1 : 0);
+      // round launches that did work: rounds 0 .. end-1 (the stop round's
+      // launch also streams the matrix)
+      uint32_t transforms = fin.end;
       double tot = 0.0;
       for (uint32_t k = 0; k < transforms && 2 + 2 * k + 1 < ev.size(); k++) {
         (void)hipEventElapsedTime(&ms, ev[2 + 2 * k], ev[2 + 2 * k + 1]);

@@ -62,7 +62,7 @@ def read_state(state) -> dict:
     raw = bytes(state.cpu().numpy().tobytes())
     s = _lib.st_state.from_buffer_copy(raw)
     return dict(done=s.done, round=s.round, iters=s.iters, stop=s.stop,
-                eigen_val=s.lambda_, max=s.max)
+                eigen_val=s.lambda_, max=s.max, end=s.end)
 
 
 # --------------------------------------------------------------------------
@@ -126,6 +126,19 @@ def scale_rowsum(mat, s_cur, s_next=None, row0: int = 0,
     _lib.check(getattr(_lib.load(), f"st_scale_rowsum_{_sfx(mat)}")(
         _ptr(mat), _ptr(s_cur), _ptr(s_next), nrows, ncols, row0, semantics,
         _ptr(state), _stream(mat.device)), "scale_rowsum")
+
+
+def round(mat, s_cur, s_next, v, state, row0: int = 0, eps: float = 1e-3, k: int = 0,
+          max_itr: int = _lib.ST_MAX_ITR, semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """One whole round k in one launch (``st_round_*``): stats of the full
+    s_cur, v update of the local rows, in-place transform, s_next."""
+    _check_cuda(mat, s_cur, s_next, v, state)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    assert s_cur.numel() >= ncols and v.numel() >= row0 + nrows and s_next.numel() >= nrows
+    _lib.check(getattr(_lib.load(), f"st_round_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(s_next), _ptr(v), nrows, ncols, row0, eps, k,
+        max_itr, semantics, _ptr(state), _stream(mat.device)), "round")
 
 
 def epilogue(s, v, state, eps: float, max_itr: int = _lib.ST_MAX_ITR,

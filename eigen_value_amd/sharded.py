@@ -2,15 +2,17 @@
 
 North-star layout (BASELINE.json): for N beyond one GPU's HBM, rank p of P
 owns the contiguous rows ``[p*chunk, p*chunk + nrows_p)`` of A, with
-``chunk = ceil(N/P)``.  Per round:
+``chunk = ceil(N/P)``.  Per round k:
 
-1. local fused kernel: ``A_p <- D^-1 A_p D`` (needs the FULL s_k for the
-   column scale) and ``s_{k+1}[local rows]``;
-2. ONE all-gather of the N-length row-sum vector (N*b/P bytes in per rank);
-3. every rank runs the O(N) epilogue redundantly on the identical gathered
-   vector (max, eigenvector, cyclic stop, λ) — deterministic kernels on
-   bitwise-identical input, so all ranks agree on ``done`` without a
-   further collective.
+1. ONE local launch (``st_round_*``): from the full, gathered s_k every
+   rank derives m_k and the stop flag (order-independent reductions over
+   bitwise-identical input, so all ranks agree without a further
+   collective), updates its own rows of the eigenvector accumulator,
+   transforms its row block ``A_p <- D_k^-1 A_p D_k`` in place and writes
+   ``s_{k+1}[local rows]`` into its slot of the padded vector;
+2. ONE all-gather of that vector (N*b/P bytes in per rank, over xGMI).
+
+At the end one more all-gather assembles the eigenvector slices.
 
 The reference has no distributed code at all ("Parallelism
 strategies ... none"); this is the exchange north_star asks for.  The
@@ -83,6 +85,10 @@ class HipShardOps:
     def epilogue(self, s, v, state, eps, max_itr, semantics):
         self.dev.epilogue(s, v, state, eps, max_itr, semantics)
 
+    def round(self, mat, s_cur, s_next, v, row0, eps, k, max_itr, semantics, state):
+        self.dev.round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
+                       max_itr=max_itr, semantics=semantics, state=state)
+
     def read_state(self, state) -> dict:
         return self.dev.read_state(state)
 
@@ -112,17 +118,21 @@ class ShardedSimilarityTransform:
         world = dist.get_world_size(group) if dist.is_initialized() else 1
         rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.part = row_block(n, world, rank)
+        if row_block(n, world, world - 1).nrows == 0:
+            raise ValueError(f"n={n} leaves a rank of {world} without rows")
         self.ops = ops or HipShardOps()
         p = self.part
         self.s = [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(2)]
-        self.v = self.ops.empty((n,), self.dtype)
+        self.v = self.ops.empty((p.world * p.chunk,), self.dtype)
         self.state = self.ops.new_state()
         self.mat = None
+        self.k = 0
+        self.cur = 0
 
     # local slot of a gathered vector
     def _slot(self, s):
         p = self.part
-        return s[p.rank * p.chunk:(p.rank + 1) * p.chunk]
+        return s[p.rank * p.chunk:p.rank * p.chunk + p.nrows]
 
     def load(self, kind: str = "hilbert", seed: int = 0, mat=None):
         """Generate (or adopt) this rank's row block."""
@@ -135,27 +145,34 @@ class ShardedSimilarityTransform:
         return self.mat
 
     def gather(self, s):
-        if self.part.world > 1:
-            _allgather(s, self._slot(s), self.group)
+        """All-gather the padded per-rank slots of s (one RCCL call)."""
+        p = self.part
+        if p.world > 1:
+            _allgather(s, s[p.rank * p.chunk:(p.rank + 1) * p.chunk], self.group)
 
     def start(self):
-        """v = 1, state = 0, s_0 = rowsum(A_0) gathered (K0)."""
-        p = self.part
+        """v = 1, state = 0, s_0 = rowsum(A_0) gathered (the initial pass)."""
         self.ops.reset_state(self.state)
         self.ops.fill(self.v, 1.0)
-        self.ops.rowsum(self.mat, self._slot(self.s[0])[:p.nrows])
+        self.ops.rowsum(self.mat, self._slot(self.s[0]))
         self.gather(self.s[0])
         self.cur = 0
+        self.k = 0
 
     def round(self, eps: float, max_itr: int):
-        """One round: epilogue(s_k) then fused transform + row sums + gather."""
+        """Round k: one fused launch (stats of s_k, v update, transform,
+        s_{k+1}) then the all-gather of s_{k+1}."""
         p, cur = self.part, self.cur
-        s_k = self.s[cur][:p.n]
-        self.ops.epilogue(s_k, self.v, self.state, eps, max_itr, self.semantics)
-        self.ops.scale_rowsum(self.mat, s_k, self._slot(self.s[cur ^ 1])[:p.nrows],
-                              p.row0, self.semantics, self.state)
+        self.ops.round(self.mat, self.s[cur][:p.n], self._slot(self.s[cur ^ 1]), self.v,
+                       p.row0, eps, self.k, max_itr, self.semantics, self.state)
         self.gather(self.s[cur ^ 1])
         self.cur = cur ^ 1
+        self.k += 1
+
+    def eigen_vector(self):
+        """Gather the eigenvector slices (each rank updated its own rows)."""
+        self.gather(self.v)
+        return self.v[:self.n]
 
     def solve(self, eps: Optional[float] = None, max_itr: int = _lib.ST_MAX_ITR,
               batch: int = 4):
@@ -163,17 +180,14 @@ class ShardedSimilarityTransform:
         if eps is None:
             eps = 1e-3
         self.start()
-        enqueued = 0
-        while enqueued < max_itr:
-            b = min(batch, max_itr - enqueued)
+        while self.k < max_itr:
+            b = min(batch, max_itr - self.k)
             for _ in range(b):
                 self.round(eps, max_itr)
-            enqueued += b
             st = self.ops.read_state(self.state)   # synchronises this rank
             if st["done"]:
                 break
         st = self.ops.read_state(self.state)
         if not st["done"]:
             raise _lib.EigenValueError("sharded solve ended without done flag")
-        rounds = st["round"] + 1 if st["stop"] else st["round"]
-        return st["eigen_val"], self.v, st["iters"], rounds
+        return st["eigen_val"], self.eigen_vector(), st["iters"], st["end"]

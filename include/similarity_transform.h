@@ -147,7 +147,9 @@ typedef struct st_state
   uint32_t stop;   /* stop flag of the last evaluated round               */
   double lambda;   /* s[0] of the last evaluated round                    */
   double max;      /* max row sum of the last evaluated round             */
-  uint64_t pad[4];
+  uint32_t end;    /* st_round_*: 1 + the round that stopped, 0 = running */
+  uint32_t reserved;
+  uint64_t pad[3];
 } st_state;
 
 /* zero a state (hipMemsetAsync) */
@@ -202,6 +204,27 @@ int st_scale_rowsum_f64(double* d_mat, const double* d_s_cur,
                         unsigned int ncols, unsigned int row0,
                         unsigned int semantics, const st_state* d_state,
                         void* stream);
+
+/* One whole round k in ONE launch (what the solve loop runs): from the full
+ * row-sum vector s_cur = s_k (length ncols), for the local rows
+ * r in [0,nrows) (global row0 + r):
+ *   m_k = max(0, max s_k), v[row0+r] *= s_k[row0+r]/m_k, stop_k = all
+ *   |s_k[i]-s_k[i+1]| < eps (cyclic for ST_SEM_SYCL), lambda = s_k[0],
+ *   A <- D_k^-1 A D_k in place and s_next[r] = row sums of the stored A.
+ * d_v is the FULL eigenvector accumulator (only the local rows are
+ * written).  k is the round index (0-based); d_state->end = k+1 once the
+ * round stops or k+1 == max_itr, and launches for later rounds are no-ops.
+ * d_state must be zeroed (st_state_reset) before round 0. */
+int st_round_f32(float* d_mat, const float* d_s_cur, float* d_s_next,
+                 float* d_v, unsigned int nrows, unsigned int ncols,
+                 unsigned int row0, float eps, unsigned int k,
+                 unsigned int max_itr, unsigned int semantics,
+                 st_state* d_state, void* stream);
+int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
+                 double* d_v, unsigned int nrows, unsigned int ncols,
+                 unsigned int row0, double eps, unsigned int k,
+                 unsigned int max_itr, unsigned int semantics,
+                 st_state* d_state, void* stream);
 
 /* Round epilogue on the full row-sum vector s[0..n): m = max(0, max s)
  * (find_max, similarity_transform.cpp:154-227), v[i] *= s[i]/m

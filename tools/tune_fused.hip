@@ -113,6 +113,8 @@ static double* g_a;
 static double* g_b;
 static double* g_s;
 static double* g_sn;
+static double* g_v;
+static st_state* g_st;
 static unsigned g_n;
 
 template <int ROWS, int U, bool NT, int BLK>
@@ -131,6 +133,23 @@ fused_variant(Timer& tm, int reps, unsigned grid_cap = 0, bool oop = false)
   double gb = 2.0 * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
   std::printf("fused  rows=%d u=%d nt=%d blk=%4d grid=%6u oop=%d  %8.4f ms  %7.1f GB/s\n",
               ROWS, U, (int)NT, BLK, grid, (int)oop, ms, gb);
+}
+
+template <int ROWS, int U, bool NT, int BLK>
+void
+round_variant(Timer& tm, int reps, unsigned grid_cap)
+{
+  const unsigned ng = g_n / ROWS;
+  const unsigned grid = grid_cap && grid_cap < ng ? grid_cap : ng;
+  auto f = [&] {
+    hipLaunchKernelGGL((k_round<double, ROWS, 2, U, 0, NT, BLK>), dim3(grid),
+                       dim3(BLK), 0, 0, g_a, g_s, g_sn, g_v, ng, 0u, g_n, 0u,
+                       0.0, 0u, 1u << 30, 0u, g_st);
+  };
+  float ms = tm.run(f, reps);
+  double gb = 2.0 * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
+  std::printf("round  rows=%d u=%d nt=%d blk=%4d grid=%6u        %8.4f ms  %7.1f GB/s\n",
+              ROWS, U, (int)NT, BLK, grid, ms, gb);
 }
 
 template <int ROWS, int U, int BLK>
@@ -160,9 +179,14 @@ main(int argc, char** argv)
   HIPCHECK(hipMalloc(&g_b, nn * 8));
   HIPCHECK(hipMalloc(&g_s, (size_t)g_n * 8));
   HIPCHECK(hipMalloc(&g_sn, (size_t)g_n * 8));
+  HIPCHECK(hipMalloc(&g_v, (size_t)g_n * 8));
+  HIPCHECK(hipMalloc(&g_st, sizeof(st_state)));
+  HIPCHECK(hipMemset(g_st, 0, sizeof(st_state)));
   hipLaunchKernelGGL((k_generate<double, kRandom>), dim3(65536), dim3(256), 0,
                      0, g_a, g_n, g_n, 0u, 0ull);
   hipLaunchKernelGGL(k_fill<double>, dim3(256), dim3(256), 0, 0, g_s,
+                     (uint64_t)g_n, 1.0);
+  hipLaunchKernelGGL(k_fill<double>, dim3(256), dim3(256), 0, 0, g_v,
                      (uint64_t)g_n, 1.0);
   HIPCHECK(hipDeviceSynchronize());
   std::printf("n=%u  matrix %.2f GiB  reps=%d\n", g_n, nn * 8.0 / (1 << 30),
@@ -207,26 +231,17 @@ main(int argc, char** argv)
     std::printf("stream_copy_nt grid=%5u     %8.4f ms  %7.1f GB/s\n", grid, ms,
                 2.0 * nn * 8 / (ms * 1e-3) / 1e9);
   }
-  // full grid (one group per workgroup)
-  fused_variant<4, 2, false, 256>(tm, reps);
-  fused_variant<2, 2, true, 256>(tm, reps);
-  fused_variant<1, 4, true, 256>(tm, reps);
-  fused_variant<2, 4, true, 256>(tm, reps);
-  fused_variant<4, 2, true, 256>(tm, reps);
-  // capped grids (grid-stride over row groups)
-  for (unsigned cap : { 512u, 1024u, 2048u }) {
-    fused_variant<1, 4, true, 256>(tm, reps, cap);
-    fused_variant<2, 2, true, 256>(tm, reps, cap);
+  for (unsigned cap : { 256u, 512u, 1024u }) {
     fused_variant<2, 4, true, 256>(tm, reps, cap);
-    fused_variant<4, 2, true, 256>(tm, reps, cap);
-    fused_variant<2, 2, false, 256>(tm, reps, cap);
-    fused_variant<1, 4, true, 512>(tm, reps, cap);
+    round_variant<1, 4, true, 256>(tm, reps, cap);
+    round_variant<2, 2, true, 256>(tm, reps, cap);
+    round_variant<2, 4, true, 256>(tm, reps, cap);
+    round_variant<4, 2, true, 256>(tm, reps, cap);
+    round_variant<4, 4, true, 256>(tm, reps, cap);
+    round_variant<2, 4, false, 256>(tm, reps, cap);
+    round_variant<2, 4, true, 512>(tm, reps, cap);
+    round_variant<1, 8, true, 256>(tm, reps, cap);
   }
-  // out of place (ping-pong)
-  fused_variant<2, 2, true, 256>(tm, reps, 0, true);
-  fused_variant<2, 2, true, 256>(tm, reps, 1024, true);
-  fused_variant<1, 4, true, 256>(tm, reps, 1024, true);
-  fused_variant<2, 2, false, 256>(tm, reps, 1024, true);
   rowsum_variant<1, 2, 256>(tm, reps);
   rowsum_variant<2, 4, 512>(tm, reps);
   rowsum_variant<2, 4, 256>(tm, reps, 1024);
