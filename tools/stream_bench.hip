@@ -81,6 +81,32 @@ k_stream(d2* a, d2* b, size_t n2, double f, double* sink)
     sink[0] = acc;
 }
 
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+// in-place stream through buffer descriptors with explicit cache-policy aux
+// bits on the load (LA) and the store (SA): 1 = sc0, 2 = nt, 16 = sc1
+template <int BLK, int U, int LA, int SA>
+__global__ __launch_bounds__(BLK) void
+k_stream_buf(d2* a, size_t n2, double f)
+{
+  const size_t per = n2 / gridDim.x; // n2 is a multiple of grid*BLK*U
+  d2* base = a + (size_t)blockIdx.x * per;
+  __amdgpu_buffer_rsrc_t r =
+    __builtin_amdgcn_make_buffer_rsrc(base, 0, (int)(per * 16), 0x00020000);
+  for (uint32_t i = threadIdx.x; i < per; i += BLK * U) {
+    u4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      x[u] = __builtin_amdgcn_raw_buffer_load_b128(r, (i + u * BLK) * 16, 0, LA);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      d2 y = __builtin_bit_cast(d2, x[u]) * f;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, y), r,
+                                             (i + u * BLK) * 16, 0, SA);
+    }
+  }
+}
+
 struct Bench
 {
   d2 *a, *b;
@@ -114,6 +140,38 @@ struct Bench
                 CHUNK ? "chunk" : "stride", grid, t[t.size() / 2],
                 bytes / (t[t.size() / 2] * 1e-3) / 1e9);
   }
+  template <int BLK, int U, int LA, int SA>
+  void runbuf(unsigned grid)
+  {
+    auto f = [&] {
+      hipLaunchKernelGGL((k_stream_buf<BLK, U, LA, SA>), dim3(grid), dim3(BLK),
+                         0, 0, a, n2, 1.0);
+    };
+    f();
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < reps; r++) {
+      HIPCHECK(hipEventRecord(e0));
+      f();
+      HIPCHECK(hipEventRecord(e1));
+      HIPCHECK(hipEventSynchronize(e1));
+      float ms;
+      HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+      t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    std::printf("inbuf  blk=%4d u=%d la=%2d sa=%2d grid=%5u  %8.4f ms  %7.1f GB/s\n",
+                BLK, U, LA, SA, grid, t[t.size() / 2],
+                2.0 * n2 * 16 / (t[t.size() / 2] * 1e-3) / 1e9);
+  }
+  template <int LA, int SA>
+  void bufgrids()
+  {
+    for (unsigned g : { 256u, 512u, 1024u }) {
+      runbuf<256, 4, LA, SA>(g);
+      runbuf<256, 2, LA, SA>(g);
+    }
+  }
   template <int BLK, int U, int POL, int MODE>
   void grids()
   {
@@ -139,19 +197,19 @@ main(int argc, char** argv)
   HIPCHECK(hipEventCreate(&B.e0));
   HIPCHECK(hipEventCreate(&B.e1));
   std::printf("buffer %zu MiB, reps %d\n", mib, B.reps);
-  B.grids<256, 1, 1, 0>();
-  B.grids<256, 2, 1, 0>();
   B.grids<256, 4, 1, 0>();
-  B.grids<256, 8, 1, 0>();
-  B.grids<512, 2, 1, 0>();
-  B.grids<512, 4, 1, 0>();
-  B.grids<1024, 2, 1, 0>();
-  B.grids<256, 4, 0, 0>();
-  B.grids<512, 4, 0, 0>();
-  B.grids<256, 4, 1, 1>();
-  B.grids<512, 4, 1, 1>();
-  B.grids<256, 4, 0, 1>();
+  B.grids<256, 2, 1, 0>();
+  B.bufgrids<0, 0>();
+  B.bufgrids<2, 2>();
+  B.bufgrids<2, 18>();
+  B.bufgrids<18, 18>();
+  B.bufgrids<16, 16>();
+  B.bufgrids<17, 17>();
+  B.bufgrids<19, 19>();
+  B.bufgrids<3, 3>();
+  B.bufgrids<2, 16>();
+  B.bufgrids<0, 2>();
+  B.bufgrids<2, 0>();
   B.grids<256, 4, 1, 2>();
-  B.grids<256, 8, 0, 2>();
   return 0;
 }
