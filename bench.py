@@ -24,7 +24,9 @@ round.  `value` = algorithmic bytes of all ranks / max-over-ranks time
 Extra objects on the JSON line: `roofline` (fused kernel, HIP events on
 the launch stream), `cpu_baseline` (the CPU oracle's 3-pass schedule on
 the host cores, rank 0 at N=1), `solve` (the reference-semantics solve to
-convergence: rounds, λ), `north_star` (32768x32768 random fp64, 1 GPU).
+convergence: rounds, λ), `matrix_free` (the read-only form of the same
+iteration, SURVEY.md §8f item 1, priced against its own N^2*b bytes),
+`north_star` (32768x32768 random fp64, 1 GPU, both forms).
 """
 from __future__ import annotations
 
@@ -92,16 +94,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    p = sh.part
     for k in range(steps):
-        cur = sh.cur
-        ev[k][0].record()
-        sh.ops.round(sh.mat, sh.s[cur][:p.n], sh._slot(sh.s[cur ^ 1]), sh.v, p.row0,
-                     0.0, sh.k, 2**31, sh.semantics, sh.state)
-        ev[k][1].record()
-        sh.gather(sh.s[cur ^ 1])
-        sh.cur = cur ^ 1
-        sh.k += 1
+        sh.round(0.0, 2**31, events=ev[k])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -171,6 +165,21 @@ def main():
                 "bytes_per_launch": bytes_round_local,
                 "traffic_source": None if traffic is None else traffic[1]}
 
+    # ---- the matrix-free form on the same workload (N^2*b per round) -----
+    mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
+    mf.load(args.kind)
+    lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=8)
+    el_mf, k_mf = timed_rounds(mf, args.steps, args.warmup, torch, dist, world)
+    by_mf_local = 1.0 * p.nrows * n * b
+    matrix_free = {"ms_per_iteration": round(el_mf / args.steps * 1e3, 5),
+                   "value": round(1.0 * n * n * b * args.steps / el_mf / 1e9, 2),
+                   "kernel_ms_avg": round(k_mf, 5),
+                   "achieved": round(by_mf_local / (k_mf * 1e-3) / 1e9, 1),
+                   "frac": round(by_mf_local / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "bytes_per_round": 1.0 * n * n * b, "solve_iter_count": it_mf,
+                   "eigen_val": lam_mf}
+    del mf
+
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
@@ -180,7 +189,7 @@ def main():
                       "bytes_per_round": bytes_round_total, "parallelism": f"rowblock{world}",
                       "baseline_config": "configs[1]: 8192x8192 Hilbert fp64, 1xMI355X"
                       if world == 1 else "configs[3]-style row-block sharding, weak-scaled"},
-           "roofline": roofline, "solve": solve}
+           "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
     del sh
     torch.cuda.empty_cache()
 
@@ -200,6 +209,20 @@ def main():
                              "traffic": None if tr is None else tr[0],
                              "solve_iter_count": it_ns, "eigen_val": lam_ns}
         del ns
+        torch.cuda.empty_cache()
+        # the matrix-free form on the same 32768^2 input (N^2*b per round)
+        mf = sharded.ShardedSimilarityTransform(32768, torch.float64, matrix_free=True)
+        mf.load("random", seed=0)
+        lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=4)
+        el_mf, k_mf = timed_rounds(mf, 20, 3, torch, dist, 1)
+        by_mf = 1.0 * 32768 * 32768 * 8
+        out["north_star"]["matrix_free"] = {
+            "ms_per_iteration": round(el_mf / 20 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
+            "achieved": round(by_mf / (k_mf * 1e-3) / 1e9, 1),
+            "frac": round(by_mf / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "bytes_per_round": by_mf, "solve_iter_count": it_mf,
+            "eigen_val_rel_diff_vs_transform": abs(lam_mf - lam_ns) / lam_ns}
+        del mf
         torch.cuda.empty_cache()
 
     # ---- CPU baseline (rank 0, N = 1) ------------------------------------

@@ -18,6 +18,7 @@ HEADER = os.path.join(REPO_DIR, "include", "similarity_transform.h")
 ST_SEM_SYCL = 0
 ST_SEM_MAINPY = 1
 ST_FLAG_TIME_KERNELS = 1
+ST_FLAG_MATRIX_FREE = 2
 ST_MAX_ITR = 1000
 
 DTYPE_F32 = 0
@@ -127,8 +128,10 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"st_epilogue_{sfx}").argtypes = [P, P, u32, T, u32, u32, P, P]
         getattr(L, f"st_round_{sfx}").argtypes = [P, P, P, P, u32, u32, u32, T, u32, u32,
                                                   u32, P, P]
+        getattr(L, f"st_mfree_round_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, T, u32,
+                                                        u32, u32, P, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
-                     "fill", "rowsum", "scale_rowsum", "epilogue", "round"):
+                     "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32

@@ -433,6 +433,203 @@ k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 }
 
 // ---------------------------------------------------------------------------
+// matrix-free round: the same iteration without ever
+// writing the matrix.  With v the eigenvector accumulator, the transformed
+// matrix of round k is A_k = X^-1 A_0 X for X = diag(x), x ∝ Π_{j<k} s_j,
+// so its row sums are s_k = (A_0 x) ⊘ x (scale-invariant in x).  Launch k
+// (k >= 1; launch 0 is the plain row-sum pass) therefore:
+//   * derives m_{k-1}, stop_{k-1} from s_{k-1} (every workgroup, as k_round)
+//   * writes v_{k-1} = v_{k-2} * (s_{k-1} / m_{k-1})   (ALL n entries, split
+//     over the workgroups: every rank of a sharded solve keeps the full v)
+//   * computes s_k[r] = (Σ_c A_0[r][c] x[c]) / x[r] for its rows with
+//     x = v_{k-2} ∘ s_{k-1} (∝ v_{k-1}: no division in the sweep)
+// and records round k-1 in `state` (end = k when round k-1 stops).  Launch
+// j exits at once if end != 0 && end < j.  A_0 is read once per round:
+// N^2*b bytes instead of the transform's 2*N^2*b.
+// ---------------------------------------------------------------------------
+template <typename T, int R, int W, int U, bool NT, int BLK, bool STATS>
+__device__ __forceinline__ void
+mfree_group(const T* a0, const T* __restrict__ s_prev,
+            const T* __restrict__ v_prev, T* __restrict__ s_next,
+            uint32_t rbase, uint32_t ncols, uint32_t row0, bool cyclic, T eps,
+            T& mx, int& ok, T (*red)[4])
+{
+  using V = typename vec<T, W>::type;
+  const uint32_t nv = ncols / W;
+  const V* sv = reinterpret_cast<const V*>(s_prev);
+  const V* vv = reinterpret_cast<const V*>(v_prev);
+  const V* rows[R];
+  T acc[R];
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    rows[j] = reinterpret_cast<const V*>(a0 + (size_t)(rbase + j) * ncols);
+    acc[j] = (T)0;
+  }
+  auto body = [&](uint32_t c, auto ucount) {
+    constexpr int UU = decltype(ucount)::value;
+    V x[UU][R];
+    V sc[UU], xs[UU];
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        x[u][j] = ld<V, NT>(rows[j] + c + u * BLK);
+#pragma unroll
+    for (int u = 0; u < UU; u++) {
+      sc[u] = sv[c + u * BLK];
+      xs[u] = vv[c + u * BLK] * sc[u];
+    }
+    if constexpr (STATS) {
+#pragma unroll
+      for (int u = 0; u < UU; u++) {
+        const uint32_t q = c + u * BLK;
+        T e[W + 1];
+        if constexpr (W == 1) {
+          e[0] = sc[u];
+        } else {
+#pragma unroll
+          for (int i = 0; i < W; i++)
+            e[i] = sc[u][i];
+        }
+        const uint32_t nxt = (q + 1) * W;
+        const bool has_next = nxt < ncols || cyclic;
+        e[W] = s_prev[nxt < ncols ? nxt : 0];
+#pragma unroll
+        for (int i = 0; i < W; i++) {
+          mx = e[i] > mx ? e[i] : mx;
+          if (i < W - 1 || has_next) {
+            const T d = e[i] - e[i + 1];
+            ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0;
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UU; u++)
+#pragma unroll
+      for (int j = 0; j < R; j++) {
+        if constexpr (W == 1) {
+          acc[j] = __builtin_fma(x[u][j], xs[u], acc[j]);
+        } else {
+#pragma unroll
+          for (int i = 0; i < W; i++)
+            acc[j] = __builtin_fma(x[u][j][i], xs[u][i], acc[j]);
+        }
+      }
+  };
+  uint32_t c = threadIdx.x;
+  for (; c + (U - 1) * BLK < nv; c += U * BLK)
+    body(c, std::integral_constant<int, U>{});
+  if constexpr (U > 1)
+    for (; c < nv; c += BLK)
+      body(c, std::integral_constant<int, 1>{});
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    T t = wave_sum(acc[j]);
+    if (lane == 0)
+      red[wave][j] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    T t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < BLK / 64; w++)
+      t += red[w][threadIdx.x];
+    const uint32_t r = row0 + rbase + threadIdx.x;
+    s_next[rbase + threadIdx.x] = t / (v_prev[r] * s_prev[r]);
+  }
+  __syncthreads();
+}
+
+template <typename T, int ROWS, int W, int U, bool NT, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_mfree(const T* a0, const T* __restrict__ s_prev, T* __restrict__ s_next,
+        const T* __restrict__ v_prev, T* __restrict__ v_cur, uint32_t ng_main,
+        uint32_t nrem, uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+        uint32_t max_itr, uint32_t semantics, st_state* state)
+{
+  static_assert(ROWS <= 4, "red[] holds 4 rows");
+  {
+    const uint32_t e =
+      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0 && e < k)
+      return;
+  }
+  __shared__ T red[BLK / 64][4];
+  __shared__ T mx_sh[BLK / 64];
+  __shared__ T m_sh;
+  const bool cyclic = semantics == ST_SEM_SYCL;
+  const uint32_t ngroups = ng_main + nrem;
+  T mx = (T)0;
+  int ok = 1;
+  T dmx = 0;
+  int dok = 1;
+  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+    const bool first = g == blockIdx.x;
+    if (g < ng_main) {
+      if (first)
+        mfree_group<T, ROWS, W, U, NT, BLK, true>(a0, s_prev, v_prev, s_next,
+                                                  g * ROWS, ncols, row0,
+                                                  cyclic, eps, mx, ok, red);
+      else
+        mfree_group<T, ROWS, W, U, NT, BLK, false>(a0, s_prev, v_prev, s_next,
+                                                   g * ROWS, ncols, row0,
+                                                   cyclic, eps, dmx, dok, red);
+    } else {
+      const uint32_t rb = ng_main * ROWS + (g - ng_main);
+      if (first)
+        mfree_group<T, 1, W, U, NT, BLK, true>(a0, s_prev, v_prev, s_next, rb,
+                                               ncols, row0, cyclic, eps, mx, ok,
+                                               red);
+      else
+        mfree_group<T, 1, W, U, NT, BLK, false>(a0, s_prev, v_prev, s_next, rb,
+                                                ncols, row0, cyclic, eps, dmx,
+                                                dok, red);
+    }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0)
+    mx_sh[threadIdx.x >> 6] = mx;
+  const int stop = __syncthreads_and(ok);
+  if (threadIdx.x == 0) {
+    T m = mx_sh[0];
+#pragma unroll
+    for (int w = 1; w < BLK / 64; w++)
+      m = mx_sh[w] > m ? mx_sh[w] : m;
+    m_sh = m;
+  }
+  __syncthreads();
+  const T m = m_sh;
+  // v_{k-1} = v_{k-2} * (s_{k-1} / m_{k-1}) over the FULL vector (cpp:260)
+  {
+    const uint32_t per = (ncols + gridDim.x - 1) / gridDim.x;
+    const uint32_t lo = blockIdx.x * per;
+    const uint32_t hi = lo + per < ncols ? lo + per : ncols;
+    for (uint32_t i = lo + threadIdx.x; i < hi; i += BLK)
+      v_cur[i] = v_prev[i] * (s_prev[i] / m);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const uint32_t rk = k - 1; // the round evaluated by this launch
+    state->lambda = (double)s_prev[0];
+    state->max = (double)m;
+    state->stop = stop ? 1u : 0u;
+    state->round = rk;
+    if (stop) {
+      state->iters = semantics == ST_SEM_SYCL ? rk : rk + 1;
+      state->end = k;
+      state->done = 1u;
+    } else if (k >= max_itr) {
+      state->iters = max_itr;
+      state->end = k;
+      state->done = 1u;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // round epilogue: one workgroup over the full row-sum vector
 // ---------------------------------------------------------------------------
 template <typename T>

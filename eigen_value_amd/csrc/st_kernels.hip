@@ -38,14 +38,26 @@ check_launch(const char* what)
   return 0;
 }
 
-// Tuned shape of the fused stream (tools/tune_fused.hip, tools/stream_bench
-// .hip; profiles/r01_tuning.md): 2 rows per group, 4 column chunks of 16 B
-// in flight per lane per row, non-temporal matrix loads/stores, at most
-// kGridCap workgroups (2 per CU) striding over the row groups.
+// Tuned shapes (tools/tune_fused.hip, tools/stream_bench.hip;
+// profiles/r01_tuning.md).  The in-place read+write stream peaks with few
+// streams in flight: 2 rows per group, 2 column chunks of 16 B per lane per
+// row, non-temporal matrix loads/stores, one 256-thread workgroup per CU
+// striding over the row groups for matrices >= 1 GiB (2 per CU below).
+// The read-only matrix-free sweep peaks at 2 workgroups per CU with 4
+// chunks in flight.
 constexpr int kRows = 2;
-constexpr int kUnroll = 4;
+constexpr int kUnroll = 2;
 constexpr bool kNontemporal = true;
 constexpr uint32_t kGridCap = 512;
+constexpr int kMfRows = 2;
+constexpr int kMfUnroll = 4;
+constexpr uint32_t kMfGridCap = 512;
+
+inline uint32_t
+round_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return (size_t)nrows * ncols * elem >= ((size_t)1 << 30) ? 256u : 512u;
+}
 
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER>
 void
@@ -106,7 +118,8 @@ launch_round_cfg(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
 {
   const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
   const uint32_t ng = ng_main + nrem;
-  const uint32_t grid = ng < kGridCap ? ng : kGridCap;
+  const uint32_t cap = round_grid_cap(nrows, ncols, sizeof(T));
+  const uint32_t grid = ng < cap ? ng : cap;
   hipLaunchKernelGGL((dev::k_round<T, ROWS, W, kUnroll, ORDER, kNontemporal>),
                      dim3(grid), dim3(kBlock), 0, stream, a, s_cur, s_next, v,
                      ng_main, nrem, ncols, row0, eps, k, max_itr, semantics,
@@ -129,7 +142,62 @@ launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                                          stream);
 }
 
+template <typename T, int ROWS, int W>
+void
+launch_mfree_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
+                 T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,
+                 T eps, uint32_t k, uint32_t max_itr, uint32_t semantics,
+                 st_state* st, hipStream_t stream)
+{
+  const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
+  const uint32_t ng = ng_main + nrem;
+  const uint32_t grid = ng < kMfGridCap ? ng : kMfGridCap;
+  hipLaunchKernelGGL((dev::k_mfree<T, ROWS, W, kMfUnroll, kNontemporal>),
+                     dim3(grid), dim3(kBlock), 0, stream, a0, s_prev, s_next,
+                     v_prev, v_cur, ng_main, nrem, ncols, row0, eps, k,
+                     max_itr, semantics, st);
+}
+
 } // namespace
+
+template <typename T>
+int
+launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
+             T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+             uint32_t k, uint32_t max_itr, uint32_t semantics, st_state* st,
+             hipStream_t stream)
+{
+  ST_REQUIRE(a0 && s_prev && s_next && v_prev && v_cur && st,
+             "mfree: null pointer");
+  ST_REQUIRE(nrows > 0 && ncols > 0, "mfree: empty block");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "mfree: bad semantics %u", semantics);
+  ST_REQUIRE(k >= 1 && max_itr > 0, "mfree: launch index k must be >= 1");
+  ST_REQUIRE(v_prev != v_cur, "mfree: v_prev and v_cur must differ");
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && aligned16(a0) && aligned16(s_prev) &&
+                      aligned16(v_prev);
+  const bool small = nrows < 2 * kMfGridCap;
+  if (vec_ok) {
+    if (small)
+      launch_mfree_cfg<T, 1, W>(a0, s_prev, s_next, v_prev, v_cur, nrows,
+                                ncols, row0, eps, k, max_itr, semantics, st,
+                                stream);
+    else
+      launch_mfree_cfg<T, kMfRows, W>(a0, s_prev, s_next, v_prev, v_cur, nrows,
+                                      ncols, row0, eps, k, max_itr, semantics,
+                                      st, stream);
+  } else {
+    if (small)
+      launch_mfree_cfg<T, 1, 1>(a0, s_prev, s_next, v_prev, v_cur, nrows,
+                                ncols, row0, eps, k, max_itr, semantics, st,
+                                stream);
+    else
+      launch_mfree_cfg<T, kMfRows, 1>(a0, s_prev, s_next, v_prev, v_cur, nrows,
+                                      ncols, row0, eps, k, max_itr, semantics,
+                                      st, stream);
+  }
+  return check_launch("mfree");
+}
 
 template <typename T>
 int
@@ -278,6 +346,14 @@ template int launch_round<double>(double*, const double*, double*, double*,
                                   uint32_t, uint32_t, uint32_t, double,
                                   uint32_t, uint32_t, uint32_t, st_state*,
                                   hipStream_t);
+template int launch_mfree<float>(const float*, const float*, float*,
+                                 const float*, float*, uint32_t, uint32_t,
+                                 uint32_t, float, uint32_t, uint32_t, uint32_t,
+                                 st_state*, hipStream_t);
+template int launch_mfree<double>(const double*, const double*, double*,
+                                  const double*, double*, uint32_t, uint32_t,
+                                  uint32_t, double, uint32_t, uint32_t,
+                                  uint32_t, st_state*, hipStream_t);
 template int launch_fill<float>(float*, uint64_t, float, hipStream_t);
 template int launch_fill<double>(double*, uint64_t, double, hipStream_t);
 
@@ -356,6 +432,18 @@ st_state_reset(st_state* d_state, void* stream)
     return st::launch_round<T>(d_mat, d_s_cur, d_s_next, d_v, nrows, ncols,    \
                                row0, eps, k, max_itr, semantics, d_state,      \
                                ST_STREAM(stream));                             \
+  }                                                                            \
+  int st_mfree_round_##SFX(const T* d_mat0, const T* d_s_prev, T* d_s_next,    \
+                           const T* d_v_prev, T* d_v_cur, unsigned int nrows,  \
+                           unsigned int ncols, unsigned int row0, T eps,       \
+                           unsigned int k, unsigned int max_itr,               \
+                           unsigned int semantics, st_state* d_state,          \
+                           void* stream)                                       \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_mfree<T>(d_mat0, d_s_prev, d_s_next, d_v_prev, d_v_cur,  \
+                               nrows, ncols, row0, eps, k, max_itr, semantics, \
+                               d_state, ST_STREAM(stream));                    \
   }                                                                            \
   int st_epilogue_##SFX(const T* d_s, T* d_v, unsigned int n, T eps,           \
                         unsigned int max_itr, unsigned int semantics,          \

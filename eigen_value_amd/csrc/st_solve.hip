@@ -61,7 +61,7 @@ struct Context
   // cached device workspaces (grown on demand, freed by destroy_queue)
   void* d_mat = nullptr;
   size_t mat_bytes = 0;
-  void* d_vec = nullptr; // [s0 | s1 | v], each vec_bytes
+  void* d_vec = nullptr; // [s0 | s1 | v | v'], each vec_bytes
   size_t vec_bytes = 0;
   st_state* d_state = nullptr;
   st_state* h_state = nullptr; // pinned, 2 slots
@@ -94,7 +94,7 @@ ensure_vectors(Context* c, size_t vec_bytes)
     ST_CHECK(hipFree(c->d_vec));
     c->d_vec = nullptr;
   }
-  ST_CHECK(hipMalloc(&c->d_vec, 3 * vec_bytes));
+  ST_CHECK(hipMalloc(&c->d_vec, 4 * vec_bytes));
   c->vec_bytes = vec_bytes;
   return 0;
 }
@@ -173,7 +173,11 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
                   reinterpret_cast<T*>((char*)c->d_vec + c->vec_bytes) };
   T* d_v = d_v_out ? d_v_out
                    : reinterpret_cast<T*>((char*)c->d_vec + 2 * c->vec_bytes);
+  // matrix-free ping-pong partner of d_v
+  T* d_v2 = reinterpret_cast<T*>((char*)c->d_vec + 3 * c->vec_bytes);
+  T* vb[2] = { d_v, d_v2 };
   const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
+  const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
   std::vector<hipEvent_t> ev; // [rowsum_a, rowsum_b, (k1_a, k1_b)*]
   auto mk = [&](hipEvent_t* e) -> int {
     ST_CHECK(hipEventCreate(e));
@@ -220,8 +224,13 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
         ev.push_back(eb);
         (void)hipEventRecord(ea, s);
       }
-      rc |= launch_round<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_v, n, n, 0,
-                            eps, k, o.max_itr, o.semantics, c->d_state, s);
+      if (mfree) // launch k+1 evaluates round k
+        rc |= launch_mfree<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], vb[k & 1],
+                              vb[(k + 1) & 1], n, n, 0, eps, k + 1, o.max_itr,
+                              o.semantics, c->d_state, s);
+      else
+        rc |= launch_round<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_v, n, n, 0,
+                              eps, k, o.max_itr, o.semantics, c->d_state, s);
       if (timed)
         (void)hipEventRecord(eb, s);
       cur ^= 1;
@@ -243,10 +252,15 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     batch_no++;
   }
   ST_CHECK(hipStreamSynchronize(s));
-  const double loop_ms = ms_since(t0);
   st_state fin;
   ST_CHECK(hipMemcpy(&fin, c->d_state, sizeof(st_state), hipMemcpyDeviceToHost));
   ST_REQUIRE(fin.done, "internal: loop ended without done flag");
+  if (mfree && (fin.end & 1u)) { // the final v_{end-1} landed in the partner
+    ST_CHECK(hipMemcpyAsync(d_v, d_v2, sizeof(T) * (size_t)n,
+                            hipMemcpyDeviceToDevice, s));
+    ST_CHECK(hipStreamSynchronize(s));
+  }
+  const double loop_ms = ms_since(t0);
 
   const auto t1 = std::chrono::steady_clock::now();
   *eigen_val = (T)fin.lambda;

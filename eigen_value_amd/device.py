@@ -141,6 +141,21 @@ def round(mat, s_cur, s_next, v, state, row0: int = 0, eps: float = 1e-3, k: int
         max_itr, semantics, _ptr(state), _stream(mat.device)), "round")
 
 
+def mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0: int = 0,
+                eps: float = 1e-3, k: int = 1, max_itr: int = _lib.ST_MAX_ITR,
+                semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """Matrix-free launch k >= 1 (``st_mfree_round_*``): round k-1's stats
+    and v_{k-1} (full vector) from s_prev, and s_k for the local rows of A_0."""
+    _check_cuda(mat0, s_prev, s_next, v_prev, v_cur, state)
+    assert mat0.is_contiguous() and mat0.dim() == 2
+    nrows, ncols = mat0.shape
+    assert s_prev.numel() >= ncols and v_prev.numel() >= ncols and v_cur.numel() >= ncols
+    assert s_next.numel() >= nrows and row0 + nrows <= ncols
+    _lib.check(getattr(_lib.load(), f"st_mfree_round_{_sfx(mat0)}")(
+        _ptr(mat0), _ptr(s_prev), _ptr(s_next), _ptr(v_prev), _ptr(v_cur), nrows, ncols,
+        row0, eps, k, max_itr, semantics, _ptr(state), _stream(mat0.device)), "mfree_round")
+
+
 def epilogue(s, v, state, eps: float, max_itr: int = _lib.ST_MAX_ITR,
              semantics: int = _lib.ST_SEM_SYCL) -> None:
     """Round epilogue: max, v *= s/m, stop test, λ = s[0], bookkeeping."""
@@ -168,22 +183,26 @@ class DeviceSolver:
 
     def solve(self, mat, *, inplace: bool = False, eps: Optional[float] = None,
               max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL, batch: int = 0,
-              time_kernels: bool = False):
+              time_kernels: bool = False, matrix_free: bool = False):
         """Returns (λ: float, v: tensor, iterations: int, stats: dict).
 
         ``mat`` is transformed in place when ``inplace`` (it is the private
-        working copy the reference makes, similarity_transform.cpp:14,19)."""
+        working copy the reference makes, similarity_transform.cpp:14,19).
+        ``matrix_free`` runs the read-only form: the
+        input is never written, so no copy is made."""
         torch = _torch()
         _check_cuda(mat)
         n = mat.shape[0]
         assert mat.shape == (n, n), "must be square"
-        work = mat if inplace else mat.clone()
+        work = mat if (inplace or matrix_free) else mat.clone()
         work = work.contiguous()
         v = torch.empty(n, dtype=mat.dtype, device=mat.device)
         ev = (ctypes.c_double if mat.dtype == torch.float64 else ctypes.c_float)()
         it = ctypes.c_uint32()
+        flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
+                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
-                              batch, _lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
+                              batch, flags)
         stats = _lib.st_stats()
         _lib.check(self.L.st_set_stream(self.q, _stream(mat.device)), "st_set_stream")
         rc = getattr(self.L, f"st_solve_device_{_sfx(mat)}")(

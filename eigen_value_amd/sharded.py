@@ -89,6 +89,11 @@ class HipShardOps:
         self.dev.round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
                        max_itr=max_itr, semantics=semantics, state=state)
 
+    def mfree_round(self, mat0, s_prev, s_next, v_prev, v_cur, row0, eps, k, max_itr,
+                    semantics, state):
+        self.dev.mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0=row0,
+                             eps=eps, k=k, max_itr=max_itr, semantics=semantics)
+
     def read_state(self, state) -> dict:
         return self.dev.read_state(state)
 
@@ -108,7 +113,7 @@ class ShardedSimilarityTransform:
     """The round loop of similarity_transform.cpp:34-66 over P row blocks."""
 
     def __init__(self, n: int, dtype=None, group=None, ops=None,
-                 semantics: int = _lib.ST_SEM_SYCL):
+                 semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -122,8 +127,11 @@ class ShardedSimilarityTransform:
             raise ValueError(f"n={n} leaves a rank of {world} without rows")
         self.ops = ops or HipShardOps()
         p = self.part
+        self.matrix_free = matrix_free
         self.s = [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(2)]
-        self.v = self.ops.empty((p.world * p.chunk,), self.dtype)
+        self.vb = [self.ops.empty((p.world * p.chunk,), self.dtype)
+                   for _ in range(2 if matrix_free else 1)]
+        self.v = self.vb[0]
         self.state = self.ops.new_state()
         self.mat = None
         self.k = 0
@@ -159,18 +167,32 @@ class ShardedSimilarityTransform:
         self.cur = 0
         self.k = 0
 
-    def round(self, eps: float, max_itr: int):
+    def round(self, eps: float, max_itr: int, events=None):
         """Round k: one fused launch (stats of s_k, v update, transform,
-        s_{k+1}) then the all-gather of s_{k+1}."""
-        p, cur = self.part, self.cur
-        self.ops.round(self.mat, self.s[cur][:p.n], self._slot(self.s[cur ^ 1]), self.v,
-                       p.row0, eps, self.k, max_itr, self.semantics, self.state)
+        s_{k+1}) then the all-gather of s_{k+1}.  Matrix-free: launch k+1
+        (round k's stats and v_k over the full vector, s_{k+1} = (A_0 x) ⊘ x
+        for the local rows) then the same all-gather."""
+        p, cur, k = self.part, self.cur, self.k
+        if events is not None:
+            events[0].record()
+        if self.matrix_free:
+            self.ops.mfree_round(self.mat, self.s[cur][:p.n], self._slot(self.s[cur ^ 1]),
+                                 self.vb[k & 1][:p.n], self.vb[(k + 1) & 1][:p.n], p.row0,
+                                 eps, k + 1, max_itr, self.semantics, self.state)
+        else:
+            self.ops.round(self.mat, self.s[cur][:p.n], self._slot(self.s[cur ^ 1]), self.v,
+                           p.row0, eps, k, max_itr, self.semantics, self.state)
+        if events is not None:
+            events[1].record()
         self.gather(self.s[cur ^ 1])
         self.cur = cur ^ 1
         self.k += 1
 
-    def eigen_vector(self):
-        """Gather the eigenvector slices (each rank updated its own rows)."""
+    def eigen_vector(self, end: Optional[int] = None):
+        """The eigenvector: matrix-free ranks hold it whole (buffer of the
+        stopping launch); otherwise gather the row slices."""
+        if self.matrix_free:
+            return self.vb[(end or self.k) & 1][:self.n]
         self.gather(self.v)
         return self.v[:self.n]
 
@@ -190,4 +212,4 @@ class ShardedSimilarityTransform:
         st = self.ops.read_state(self.state)
         if not st["done"]:
             raise _lib.EigenValueError("sharded solve ended without done flag")
-        return st["eigen_val"], self.eigen_vector(), st["iters"], st["end"]
+        return st["eigen_val"], self.eigen_vector(st["end"]), st["iters"], st["end"]

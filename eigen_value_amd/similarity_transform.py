@@ -74,7 +74,8 @@ class EigenValue:
     # ------------------------------------------------------------------
     def similarity_transform_ex(self, mat: np.ndarray, *, eps: Optional[float] = None,
                                 max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL,
-                                batch: int = 0, time_kernels: bool = False):
+                                batch: int = 0, time_kernels: bool = False,
+                                matrix_free: bool = False):
         """Extended call: options + statistics (``max_eigen_value_ex``).
 
         Returns ``(λ, v, ts_ms, iterations, stats_dict)``."""
@@ -83,8 +84,10 @@ class EigenValue:
         mat = np.ascontiguousarray(mat)
         if mat.dtype not in (np.float32, np.float64):
             raise TypeError("float32 or float64 matrix required")
+        flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
+                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
-                              batch, _lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
+                              batch, flags)
         stats = _lib.st_stats()
         eigen_val = np.empty(1, dtype=mat.dtype)
         eigen_vec = np.empty(n, dtype=mat.dtype)

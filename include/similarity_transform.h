@@ -88,6 +88,8 @@ typedef struct st_options
 } st_options;
 
 #define ST_FLAG_TIME_KERNELS 1u /* hipEvents around every fused launch     */
+#define ST_FLAG_MATRIX_FREE 2u  /* st_mfree_round_* instead of the in-place */
+                                /* transform (input never written)         */
 
 typedef struct st_stats
 {
@@ -225,6 +227,31 @@ int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                  unsigned int row0, double eps, unsigned int k,
                  unsigned int max_itr, unsigned int semantics,
                  st_state* d_state, void* stream);
+
+/* Matrix-free round.  The transformed matrix of
+ * round k is X^-1 A_0 X with x ∝ the product of all previous row-sum
+ * vectors, so its row sums are (A_0 x) ⊘ x and A_0 never has to be
+ * rewritten: N^2*b bytes per round instead of 2*N^2*b.  Launch k >= 1
+ * (launch 0 is st_rowsum on A_0, giving s_0; v_prev = 1 for launch 1):
+ *   from the FULL s_prev = s_{k-1}: m, stop, lambda of round k-1 (recorded
+ *   in d_state, end = k when round k-1 stops or k == max_itr);
+ *   d_v_cur[0..ncols) = d_v_prev * (s_prev / m)   (v_{k-1}, full vector);
+ *   d_s_next[r] = (Σ_c A_0[r][c] x[c]) / x[row0+r], x = v_prev ∘ s_prev,
+ *   for the local rows (s_k).
+ * d_mat0 is read only.  v_prev/v_cur and s_prev/s_next are ping-pong
+ * buffers.  Launches after the stopping one are no-ops. */
+int st_mfree_round_f32(const float* d_mat0, const float* d_s_prev,
+                       float* d_s_next, const float* d_v_prev, float* d_v_cur,
+                       unsigned int nrows, unsigned int ncols,
+                       unsigned int row0, float eps, unsigned int k,
+                       unsigned int max_itr, unsigned int semantics,
+                       st_state* d_state, void* stream);
+int st_mfree_round_f64(const double* d_mat0, const double* d_s_prev,
+                       double* d_s_next, const double* d_v_prev,
+                       double* d_v_cur, unsigned int nrows, unsigned int ncols,
+                       unsigned int row0, double eps, unsigned int k,
+                       unsigned int max_itr, unsigned int semantics,
+                       st_state* d_state, void* stream);
 
 /* Round epilogue on the full row-sum vector s[0..n): m = max(0, max s)
  * (find_max, similarity_transform.cpp:154-227), v[i] *= s[i]/m

@@ -394,6 +394,88 @@ def test_full_size_properties(solver):
     torch.cuda.empty_cache()
 
 
+# ---------------------------------------------------------------------------
+# matrix-free form
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("kind,n", [("hilbert", 128), ("hilbert", 1000), ("hilbert", 4096),
+                                    ("random", 333), ("random", 1024), ("random", 4099),
+                                    ("random", 3)])
+def test_matrix_free_fp64_vs_oracle(eigen, orc, kind, n):
+    mat = orc.hilbert(n) if kind == "hilbert" else orc.random_matrix(n, 11)
+    lam, v, ts, itr, st = eigen.similarity_transform_ex(mat, matrix_free=True)
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL)
+    assert itr == ref.iter_count and st["rounds"] == ref.rounds_evaluated
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
+
+
+def test_matrix_free_mainpy_vs_golden(eigen, orc, golden):
+    cases, vecs, _ = golden
+    for name, case in cases.items():
+        mat = golden_input(case, orc)
+        lam, v, ts, itr, _ = eigen.similarity_transform_ex(mat, semantics=_lib.ST_SEM_MAINPY,
+                                                           matrix_free=True)
+        assert itr == case["itr"], name
+        assert abs(lam - case["eigen_val"]) <= 1e-11 * abs(case["eigen_val"]), name
+        assert np.max(np.abs(v - vecs[name])) <= 1e-11, name
+
+
+def test_matrix_free_fp32_round_counts(eigen, orc, golden):
+    p = golden[2]["hilbert_round_counts_fp32"]
+    for n, rounds in zip(p["sizes"], p["rounds"]):
+        mat = orc.hilbert(n, np.float32)
+        lam, v, ts, itr, _ = eigen.similarity_transform_ex(mat, matrix_free=True)
+        assert itr == rounds, (n, itr, rounds)
+        ref = orc.similarity_transform(mat, orc.SEM_SYCL)
+        assert abs(lam - ref.eigen_val) <= 1e-5 * ref.eigen_val
+
+
+def test_matrix_free_leaves_input_and_matches_transform(solver):
+    n = 6000
+    a = dev.generate("random", n, torch.float64, seed=2, device=DEV)
+    keep = a.clone()
+    lam, v, it, st = solver.solve(a, matrix_free=True, batch=3)
+    assert torch.equal(a, keep)                       # A_0 is never written
+    lam_t, v_t, it_t, st_t = solver.solve(a)
+    assert it == it_t and st["rounds"] == st_t["rounds"]
+    assert abs(lam - lam_t) <= 1e-12 * lam_t
+    assert (v - v_t).abs().max().item() <= 1e-12
+    lam_x, v_x, it_x, st_x = solver.solve(a, matrix_free=True, eps=0.0, max_itr=7)
+    assert it_x == 7 and st_x["rounds"] == 7 and st_x["converged"] == 0
+
+
+def _gpu_gloo_mfree_worker(rank, world, port, n, outdir):
+    import torch.distributed as dist
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sh = ShardedSimilarityTransform(n, torch.float64, matrix_free=True)
+        sh.load("hilbert")
+        lam, v, iters, rounds = sh.solve(eps=1e-3, batch=5)
+        np.save(os.path.join(outdir, f"v{rank}.npy"), v.cpu().numpy())
+        np.save(os.path.join(outdir, f"m{rank}.npy"), np.array([lam, iters, rounds]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_matrix_free_sharded_two_ranks(tmp_path, solver):
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    n = 3001
+    mp.spawn(_gpu_gloo_mfree_worker, args=(2, port, n, str(tmp_path)), nprocs=2, join=True)
+    a = dev.generate("hilbert", n, torch.float64, device=DEV)
+    lam, v, it, st = solver.solve(a, matrix_free=True)
+    for r in range(2):
+        lam_r, it_r, rounds_r = np.load(tmp_path / f"m{r}.npy")
+        assert lam_r == lam and int(it_r) == it and int(rounds_r) == st["rounds"]
+        assert np.array_equal(np.load(tmp_path / f"v{r}.npy"), to_np(v))
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess

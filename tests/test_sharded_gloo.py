@@ -99,6 +99,26 @@ class CpuShardOps:
         mat.copy_(torch.from_numpy(new))
         s_next.copy_(torch.from_numpy(self.o.rowsum(new)))
 
+    def mfree_round(self, mat0, s_prev, s_next, v_prev, v_cur, row0, eps, k, max_itr,
+                    semantics, st):
+        # the st_mfree_round_* contract, restated (numpy matmul as the GEMV)
+        e = st.get("end", 0)
+        if e and e < k:
+            return
+        sn, vp = s_prev.numpy(), v_prev.numpy()
+        m = self.o.find_max(sn)
+        v_cur.copy_(torch.from_numpy(self.o.compute_eigen_vector(sn, m, vp)))
+        ok = self.o.stop(sn, eps=sn.dtype.type(eps), cyclic=semantics == _lib.ST_SEM_SYCL)
+        rk = k - 1
+        st.update(eigen_val=float(sn[0]), max=float(m), stop=int(ok), round=rk)
+        if ok:
+            st.update(done=1, end=k, iters=rk if semantics == _lib.ST_SEM_SYCL else rk + 1)
+        elif k >= max_itr:
+            st.update(done=1, end=k, iters=max_itr)
+        x = vp * sn
+        nr = mat0.shape[0]
+        s_next.copy_(torch.from_numpy((mat0.numpy() @ x) / x[row0:row0 + nr]))
+
     def read_state(self, st):
         return dict(st)
 
@@ -109,11 +129,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, kind, dtype, semantics, outdir):
+def _worker(rank, world, port, n, kind, dtype, semantics, outdir, matrix_free=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sh = ShardedSimilarityTransform(n, dtype, ops=CpuShardOps(), semantics=semantics)
+        sh = ShardedSimilarityTransform(n, dtype, ops=CpuShardOps(), semantics=semantics,
+                                        matrix_free=matrix_free)
         sh.load(kind, seed=3)
         lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=3)
         np.save(os.path.join(outdir, f"v{rank}.npy"), v.numpy())
@@ -155,3 +176,20 @@ def test_sharded_solve_bit_identical_to_oracle(tmp_path, orc, world, n, kind, dt
         assert int(rounds) == ref.rounds_evaluated
         assert npdt(lam) == ref.eigen_val           # bit-identical on every rank
         assert np.array_equal(v, ref.eigen_vec)
+
+
+@pytest.mark.parametrize("world,n", [(2, 200), (3, 101)])
+def test_sharded_matrix_free_matches_oracle(tmp_path, orc, world, n):
+    """Matrix-free sharded loop: same rounds as the transform, λ and v to
+    fp64 rounding (the GEMV association differs from the transform's)."""
+    mp.spawn(_worker, args=(world, _free_port(), n, "random", torch.float64,
+                            _lib.ST_SEM_SYCL, str(tmp_path), True), nprocs=world, join=True)
+    ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL)
+    v0 = np.load(tmp_path / "v0.npy")
+    for r in range(world):
+        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")
+        assert int(iters) == ref.iter_count and int(rounds) == ref.rounds_evaluated
+        assert abs(lam - ref.eigen_val) <= 1e-12 * ref.eigen_val
+        v = np.load(tmp_path / f"v{r}.npy")
+        assert np.array_equal(v, v0)                      # identical on every rank
+        assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-12

@@ -152,6 +152,25 @@ round_variant(Timer& tm, int reps, unsigned grid_cap)
               ROWS, U, (int)NT, BLK, grid, ms, gb);
 }
 
+static double* g_v2;
+
+template <int ROWS, int U, bool NT, int BLK>
+void
+mfree_variant(Timer& tm, int reps, unsigned grid_cap)
+{
+  const unsigned ng = g_n / ROWS;
+  const unsigned grid = grid_cap && grid_cap < ng ? grid_cap : ng;
+  auto f = [&] {
+    hipLaunchKernelGGL((k_mfree<double, ROWS, 2, U, NT, BLK>), dim3(grid),
+                       dim3(BLK), 0, 0, g_a, g_s, g_sn, g_v, g_v2, ng, 0u, g_n,
+                       0u, 0.0, 1u, 1u << 30, 0u, g_st);
+  };
+  float ms = tm.run(f, reps);
+  double gb = 1.0 * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
+  std::printf("mfree  rows=%d u=%d nt=%d blk=%4d grid=%6u        %8.4f ms  %7.1f GB/s\n",
+              ROWS, U, (int)NT, BLK, grid, ms, gb);
+}
+
 template <int ROWS, int U, int BLK>
 void
 rowsum_variant(Timer& tm, int reps, unsigned grid_cap = 0)
@@ -180,6 +199,7 @@ main(int argc, char** argv)
   HIPCHECK(hipMalloc(&g_s, (size_t)g_n * 8));
   HIPCHECK(hipMalloc(&g_sn, (size_t)g_n * 8));
   HIPCHECK(hipMalloc(&g_v, (size_t)g_n * 8));
+  HIPCHECK(hipMalloc(&g_v2, (size_t)g_n * 8));
   HIPCHECK(hipMalloc(&g_st, sizeof(st_state)));
   HIPCHECK(hipMemset(g_st, 0, sizeof(st_state)));
   hipLaunchKernelGGL((k_generate<double, kRandom>), dim3(65536), dim3(256), 0,
@@ -230,6 +250,16 @@ main(int argc, char** argv)
     ms = tm.run(g, reps);
     std::printf("stream_copy_nt grid=%5u     %8.4f ms  %7.1f GB/s\n", grid, ms,
                 2.0 * nn * 8 / (ms * 1e-3) / 1e9);
+  }
+  for (unsigned cap : { 256u, 512u, 1024u, 2048u }) {
+    mfree_variant<1, 4, true, 256>(tm, reps, cap);
+    mfree_variant<2, 4, true, 256>(tm, reps, cap);
+    mfree_variant<4, 4, true, 256>(tm, reps, cap);
+    mfree_variant<4, 2, true, 256>(tm, reps, cap);
+    mfree_variant<2, 2, true, 256>(tm, reps, cap);
+    mfree_variant<2, 8, true, 256>(tm, reps, cap);
+    mfree_variant<2, 4, false, 256>(tm, reps, cap);
+    mfree_variant<2, 4, true, 512>(tm, reps, cap);
   }
   for (unsigned cap : { 256u, 512u, 1024u }) {
     fused_variant<2, 4, true, 256>(tm, reps, cap);
