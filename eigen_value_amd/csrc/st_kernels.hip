@@ -43,15 +43,21 @@ check_launch(const char* what)
 // streams in flight: 2 rows per group, 2 column chunks of 16 B per lane per
 // row, non-temporal matrix loads/stores, one 256-thread workgroup per CU
 // striding over the row groups for matrices >= 1 GiB (2 per CU below).
-// The read-only matrix-free sweep peaks at 2 workgroups per CU with 4
-// chunks in flight.
+// The read-only matrix-free sweep peaks with 4 rows per group, 2 chunks in
+// flight, 2 workgroups per CU for matrices >= 1 GiB (4 per CU below).
 constexpr int kRows = 2;
 constexpr int kUnroll = 2;
 constexpr bool kNontemporal = true;
 constexpr uint32_t kGridCap = 512;
-constexpr int kMfRows = 2;
-constexpr int kMfUnroll = 4;
-constexpr uint32_t kMfGridCap = 512;
+constexpr int kMfRows = 4;
+constexpr int kMfUnroll = 2;
+constexpr uint32_t kMfGridCap = 1024;
+
+inline uint32_t
+mfree_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return (size_t)nrows * ncols * elem >= ((size_t)1 << 30) ? 512u : 1024u;
+}
 
 inline uint32_t
 round_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
@@ -151,7 +157,8 @@ launch_mfree_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
 {
   const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
   const uint32_t ng = ng_main + nrem;
-  const uint32_t grid = ng < kMfGridCap ? ng : kMfGridCap;
+  const uint32_t cap = mfree_grid_cap(nrows, ncols, sizeof(T));
+  const uint32_t grid = ng < cap ? ng : cap;
   hipLaunchKernelGGL((dev::k_mfree<T, ROWS, W, kMfUnroll, kNontemporal>),
                      dim3(grid), dim3(kBlock), 0, stream, a0, s_prev, s_next,
                      v_prev, v_cur, ng_main, nrem, ncols, row0, eps, k,
@@ -176,7 +183,7 @@ launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
   constexpr int W = 16 / sizeof(T);
   const bool vec_ok = (ncols % W) == 0 && aligned16(a0) && aligned16(s_prev) &&
                       aligned16(v_prev);
-  const bool small = nrows < 2 * kMfGridCap;
+  const bool small = nrows < 2 * kMfGridCap; // keep >= 2 rows per workgroup
   if (vec_ok) {
     if (small)
       launch_mfree_cfg<T, 1, W>(a0, s_prev, s_next, v_prev, v_cur, nrows,
