@@ -67,9 +67,11 @@ def scaled_n(n1: int, world: int) -> int:
     return int(round(n1 * math.sqrt(world) / q)) * q
 
 
-def load_traffic(workload: str):
-    """Per-launch HBM bytes of the fused kernel from committed rocprofv3 PMC
-    passes (profiles/*_pmc.json, written by tools/pmc_traffic.py)."""
+def load_traffic(workload: str, kernel: str = "k_round"):
+    """Per-launch HBM bytes of a hot kernel from the committed rocprofv3 PMC
+    passes of this workload (profiles/*_pmc.json, tools/pmc_traffic.py;
+    FETCH_SIZE and WRITE_SIZE from separate passes, FETCH_SIZE doubled per
+    the gfx950 correction).  The latest round's file wins."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_pmc.json"))):
@@ -77,8 +79,11 @@ def load_traffic(workload: str):
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("workload") == workload and d.get("fused_bytes_per_launch"):
-            best = (d["fused_bytes_per_launch"], os.path.relpath(f, HERE))
+        if d.get("workload") != workload:
+            continue
+        for e in d.get("entries", []):
+            if e.get("kernel") == kernel:
+                best = (e["hbm_bytes_per_launch"], os.path.relpath(f, HERE))
     return best
 
 
@@ -140,7 +145,9 @@ def main():
     sh.load(args.kind)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=8)
+    # batch=1: the host checks the stop flag after every round, as the
+    # reference does (similarity_transform.cpp:45-50); no gated launches
+    lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=1)
     torch.cuda.synchronize()
     solve_ms = (time.perf_counter() - t0) * 1e3
     solve = {"eps": 1e-3, "iter_count": iters, "rounds_evaluated": rounds,
@@ -168,10 +175,12 @@ def main():
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
     mf.load(args.kind)
-    lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=8)
+    lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=1)
     el_mf, k_mf = timed_rounds(mf, args.steps, args.warmup, torch, dist, world)
     by_mf_local = 1.0 * p.nrows * n * b
+    tr_mf = load_traffic(workload, "k_mfree")
     matrix_free = {"ms_per_iteration": round(el_mf / args.steps * 1e3, 5),
+                   "traffic": None if tr_mf is None else tr_mf[0],
                    "value": round(1.0 * n * n * b * args.steps / el_mf / 1e9, 2),
                    "kernel_ms_avg": round(k_mf, 5),
                    "achieved": round(by_mf_local / (k_mf * 1e-3) / 1e9, 1),
@@ -197,7 +206,7 @@ def main():
     if world == 1 and not args.no_north_star:
         ns = sharded.ShardedSimilarityTransform(32768, torch.float64)
         ns.load("random", seed=0)
-        lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=4)
+        lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=1)
         ns.load("random", seed=0)
         el_ns, fused_ns = timed_rounds(ns, 20, 3, torch, dist, 1)
         by = 2.0 * 32768 * 32768 * 8
@@ -213,10 +222,12 @@ def main():
         # the matrix-free form on the same 32768^2 input (N^2*b per round)
         mf = sharded.ShardedSimilarityTransform(32768, torch.float64, matrix_free=True)
         mf.load("random", seed=0)
-        lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=4)
+        lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=1)
         el_mf, k_mf = timed_rounds(mf, 20, 3, torch, dist, 1)
         by_mf = 1.0 * 32768 * 32768 * 8
+        tr_mf = load_traffic("random32768_f64", "k_mfree")
         out["north_star"]["matrix_free"] = {
+            "traffic": None if tr_mf is None else tr_mf[0],
             "ms_per_iteration": round(el_mf / 20 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
             "achieved": round(by_mf / (k_mf * 1e-3) / 1e9, 1),
             "frac": round(by_mf / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),

@@ -40,6 +40,16 @@ for s in $STEPS; do
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
       step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
     tune)  step tune 600 ./tools/tune_fused ;;
+    profile)
+      # one workload per profiled command, so every rocprofv3 summary row
+      # belongs to a single launch shape: configs[1] and the north-star size
+      for W in "hilbert 8192" "random 32768"; do
+        set -- $W; K=$1; N=$2; D="$OUT/${K}${N}"
+        step "prof_${K}${N}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind $K --n $N --no-cpu --no-north-star
+        step "pmc_fetch_${K}${N}" 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star
+        step "pmc_write_${K}${N}" 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star
+        python3 tools/pmc_traffic.py --workload "${K}${N}_f64" --n $N --fetch "$D/pmc_fetch/run_counter_collection.csv" --write "$D/pmc_write/run_counter_collection.csv" --trace "$D/prof/run_kernel_trace.csv" --out "$D/pmc.json" | tee -a "$OUT/session.log"
+      done ;;
   esac
 done
 echo "== session done" | tee -a "$OUT/session.log"
