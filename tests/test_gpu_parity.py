@@ -476,6 +476,22 @@ def test_matrix_free_sharded_two_ranks(tmp_path, solver):
         assert np.array_equal(np.load(tmp_path / f"v{r}.npy"), to_np(v))
 
 
+def test_fp32_large_never_converges_at_reference_eps(solver):
+    """fp32 row sums ≈ N/2 at N = 16384 have an ulp (2^-10 ≈
+    9.8e-4 at 8192, 2^-9 at 16384) at the EPS scale, so the reference's fp32
+    stop test never passes and the loop runs MAX_ITR = 1000 rounds; λ still
+    agrees with the fp64 solve to fp32 precision."""
+    n = 16384
+    a32 = dev.generate("random", n, torch.float32, seed=0, device=DEV)
+    lam32, v32, it32, st32 = solver.solve(a32, inplace=True, batch=64)
+    assert it32 == 1000 and st32["converged"] == 0 and st32["rounds"] == 1000
+    a64 = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    lam64, v64, it64, _ = solver.solve(a64, inplace=True)
+    assert it64 == 3
+    assert abs(lam32 - lam64) <= 2e-6 * lam64
+    assert (v32.double() - v64).abs().max().item() <= 1e-4
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess

@@ -40,6 +40,11 @@ for s in $STEPS; do
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
       step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
     tune)  step tune 600 ./tools/tune_fused ;;
+    hilbert)
+      make -s -C tools bench_hilbert
+      step bench_hilbert_f32 300 ./tools/bench_hilbert f32
+      step bench_hilbert_f64 300 ./tools/bench_hilbert f64 ;;
+    fp32)  step fp32_study 600 python3 tools/fp32_study.py --out "$OUT/fp32_study.json" ;;
     profile)
       # one workload per profiled command, so every rocprofv3 summary row
       # belongs to a single launch shape: configs[1] and the north-star size
