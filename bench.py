@@ -57,6 +57,10 @@ def parse():
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-north-star", action="store_true")
     p.add_argument("--cpu-rounds", type=int, default=5)
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    p.add_argument("--one-gpu", action="store_true",
+                   help="rehearsal: every rank on cuda:0 (use with --backend gloo)")
     return p.parse_args()
 
 
@@ -108,7 +112,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     el = time.perf_counter() - t0
     fused = sum(a.elapsed_time(b) for a, b in ev) / steps
     if world > 1:
-        t = torch.tensor([el, fused], dtype=torch.float64, device="cuda")
+        t = torch.tensor([el, fused], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el, fused = float(t[0]), float(t[1])
     return el, fused
@@ -128,10 +133,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    dev_index = 0 if args.one_gpu else local
+    torch.cuda.set_device(dev_index)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
     _lib.load()   # fail loudly before anything else if the HIP library is missing
 
     dt = torch.float64 if args.dtype == "f64" else torch.float32
