@@ -56,7 +56,8 @@ def parse():
     p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     p.add_argument("--no-cpu", action="store_true")
     p.add_argument("--no-north-star", action="store_true")
-    p.add_argument("--cpu-rounds", type=int, default=5)
+    p.add_argument("--cpu-seconds", type=float, default=10.0,
+                   help="CPU baseline sample length (rounds are calibrated to it)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     p.add_argument("--one-gpu", action="store_true",
@@ -251,17 +252,25 @@ def main():
         threads = min(16, len(os.sched_getaffinity(0)))
         npdt = np.float64 if args.dtype == "f64" else np.float32
         mat = orc.hilbert(n, npdt) if args.kind == "hilbert" else orc.random_matrix(n, 0, npdt)
-        r = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=args.cpu_rounds,
+        # bounded sample: calibrate on 3 rounds, then ~--cpu-seconds of rounds
+        cal = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=3, nthreads=threads)
+        est = max(cal.loop_ms / 3, 1e-3)
+        rounds_cpu = int(min(5000, max(3, args.cpu_seconds * 1e3 / est)))
+        r = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=rounds_cpu,
                                      nthreads=threads)
-        # rounds evaluated = cpu_rounds row-sum passes and cpu_rounds-1 transforms;
-        # price it per round with the same 2*N^2*b accounting as `value`
-        per_round_ms = r.loop_ms / args.cpu_rounds
+        # every round = row-sum pass + stats + transform pass (the last round's
+        # transform is skipped, as in the reference loop); priced with the same
+        # 2*N^2*b accounting as `value`
+        per_round_ms = r.loop_ms / rounds_cpu
+        solve_cpu = orc.similarity_transform(mat, orc.SEM_SYCL, nthreads=threads)
         out["cpu_baseline"] = {"value": round(bytes_round_total / (per_round_ms * 1e-3) / 1e9, 3),
                                "unit": "GB/s", "ms_per_iteration": round(per_round_ms, 3),
                                "cores": threads, "kind": "port",
-                               "sample": f"{workload}, {args.cpu_rounds} rounds (eps=0) of the "
-                                         "reference's 3-pass schedule (oracle/st_oracle.c, gcc "
-                                         "-O3 OpenMP)"}
+                               "sample": f"{workload}: {rounds_cpu} rounds (eps=0, "
+                                         f"{r.loop_ms / 1e3:.1f} s) of the reference's 3-pass "
+                                         "schedule (oracle/st_oracle.c, gcc -O3, OpenMP over rows)",
+                               "solve_ms": round(solve_cpu.loop_ms, 2),
+                               "solve_iter_count": solve_cpu.iter_count}
         out["speedup_vs_cpu"] = round(out["ms_per_step"] and per_round_ms / out["ms_per_step"], 1)
 
     if rank == 0:
