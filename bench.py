@@ -18,7 +18,8 @@ Workload (config.workload): BASELINE.json configs[1], 8192x8192 Hilbert
 fp64 on one GPU.  For N GPUs the row-block sharded path runs with
 per-GPU bytes held constant (weak scaling): n = 8192*sqrt(N) rounded to a
 multiple of 64*N, rows split in contiguous blocks, one RCCL all-gather per
-round.  `value` = algorithmic bytes of all ranks / max-over-ranks time
+round.  `--strong` keeps n fixed instead (configs[3]:
+`--n 65536 --kind random --strong` on 8 GPUs).  `value` = algorithmic bytes of all ranks / max-over-ranks time
 (GB/s); `ms_per_step` = ms/iteration.
 
 Extra objects on the JSON line: `roofline` (fused kernel, HIP events on
@@ -58,6 +59,9 @@ def parse():
     p.add_argument("--no-north-star", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0,
                    help="CPU baseline sample length (rounds are calibrated to it)")
+    p.add_argument("--strong", action="store_true",
+                   help="keep n fixed for every N (strong scaling; e.g. configs[3]: "
+                        "--n 65536 --kind random --strong)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     p.add_argument("--one-gpu", action="store_true",
@@ -146,7 +150,7 @@ def main():
 
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     b = 8 if args.dtype == "f64" else 4
-    n = scaled_n(args.n, world)
+    n = args.n if args.strong else scaled_n(args.n, world)
     workload = f"{args.kind}{n}_{args.dtype}"
     sh = sharded.ShardedSimilarityTransform(n, dt)
     p = sh.part
@@ -202,12 +206,15 @@ def main():
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
-           "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "higher_is_better": True, "scaling": "strong" if args.strong else "weak",
+           "vs_baseline": None,
            "dtype": args.dtype, "data": f"synthetic ({args.kind}, generated in HBM)",
            "config": {"workload": workload, "n": n, "rows_per_gpu": p.chunk,
                       "bytes_per_round": bytes_round_total, "parallelism": f"rowblock{world}",
-                      "baseline_config": "configs[1]: 8192x8192 Hilbert fp64, 1xMI355X"
-                      if world == 1 else "configs[3]-style row-block sharding, weak-scaled"},
+                      "baseline_config": ("configs[1]: 8192x8192 Hilbert fp64, 1xMI355X"
+                                          if (world == 1 and n == 8192) else
+                                          f"row-block sharding over {world} GPU(s), "
+                                          + ("strong" if args.strong else "weak") + "-scaled")},
            "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
     del sh
     torch.cuda.empty_cache()

@@ -494,6 +494,22 @@ def test_fp32_large_never_converges_at_reference_eps(solver):
     assert (v32.double() - v64).abs().max().item() <= 1e-3
 
 
+def test_config4_size_on_one_gpu(solver):
+    """BASELINE configs[3] size, 65536² fp64 = 32 GiB (N² = 2^32 elements:
+    exercises every 64-bit index path), on one GPU: converges, residual
+    small, matrix-free agrees, and the 32 GiB row-block path with P = 1."""
+    n = 65536
+    a = dev.generate("random", n, torch.float64, seed=4, device=DEV)
+    lam_mf, v_mf, it_mf, _ = solver.solve(a, matrix_free=True)
+    r = torch.mv(a, v_mf) - lam_mf * v_mf
+    assert (r.abs().max() / (lam_mf * v_mf.abs().max())).item() < 1e-9
+    lam, v, it, _ = solver.solve(a, inplace=True)
+    assert it == it_mf and abs(lam - lam_mf) <= 1e-12 * lam
+    assert (v - v_mf).abs().max().item() <= 1e-12
+    del a, r
+    torch.cuda.empty_cache()
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess
