@@ -510,6 +510,28 @@ def test_config4_size_on_one_gpu(solver):
     torch.cuda.empty_cache()
 
 
+def test_error_paths_and_degenerate_inputs(eigen):
+    L = _lib.load()
+    one = np.ones((1, 1), np.float32)
+    ev_, vec_, it_ = np.zeros(1, np.float32), np.zeros(1, np.float32), np.zeros(1, np.uint32)
+    # dim = 0: negative return and a message, never a crash or a hang
+    assert L.max_eigen_value(eigen.sycl_q, one.ctypes.data, ev_.ctypes.data,
+                             vec_.ctypes.data, 0, it_.ctypes.data) < 0
+    assert "dim" in _lib.last_error()
+    with pytest.raises(_lib.EigenValueError):
+        eigen.similarity_transform_ex(np.ones((3, 3), np.float32), semantics=7)
+    # all-zero matrix: s = 0 everywhere -> the cyclic stop test passes at
+    # round 0 (|0 - 0| < EPS), λ = 0, as the reference's loop would
+    lam, v, ts, itr = eigen.similarity_transform(np.zeros((64, 64), np.float32))
+    assert lam == 0 and itr == 0
+    # NaN input: the stop test never passes (NaN compares false), the loop
+    # runs to max_itr and reports it — no hang
+    bad = np.ones((32, 32), np.float64)
+    bad[3, 4] = np.nan
+    lam, v, ts, itr, st = eigen.similarity_transform_ex(bad, max_itr=6)
+    assert itr == 6 and st["converged"] == 0 and np.isnan(lam)
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess

@@ -252,6 +252,14 @@ main(int argc, char** argv)
                 2.0 * nn * 8 / (ms * 1e-3) / 1e9);
   }
   for (unsigned cap : { 256u, 512u, 1024u, 2048u }) {
+    round_variant<1, 1, true, 256>(tm, reps, cap);
+    round_variant<1, 2, true, 256>(tm, reps, cap);
+    round_variant<2, 1, true, 256>(tm, reps, cap);
+    round_variant<4, 1, true, 256>(tm, reps, cap);
+    round_variant<2, 2, true, 512>(tm, reps, cap);
+    round_variant<4, 2, true, 512>(tm, reps, cap);
+  }
+  for (unsigned cap : { 256u, 512u, 1024u, 2048u }) {
     mfree_variant<1, 4, true, 256>(tm, reps, cap);
     mfree_variant<2, 4, true, 256>(tm, reps, cap);
     mfree_variant<4, 4, true, 256>(tm, reps, cap);
