@@ -97,27 +97,37 @@ def load_traffic(workload: str, kernel: str = "k_round"):
 
 
 def timed_rounds(sh, steps, warmup, torch, dist, world):
-    """Warmup + K timed rounds; returns (elapsed_s_max, fused_ms_avg)."""
+    """Warmup + K timed rounds; returns (elapsed_s_max, kernel_ms_avg).
+
+    The kernel's average launch duration comes from HIP events recorded on
+    the launch stream (torch's current stream, which the C-ABI launches on).
+    At N = 1 the timed region holds nothing but the round launches, so two
+    events bracket it (per-launch events would add ~7 us of event work to
+    every 175 us round); with N > 1 the all-gathers sit between launches, so
+    each launch is bracketed by its own pair."""
     sh.start()
     for _ in range(warmup):
         sh.round(0.0, 2**31)
     torch.cuda.synchronize()
+    per_launch = world > 1
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps)]
+          for _ in range(steps if per_launch else 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    no_events = os.environ.get("EIGEN_BENCH_NO_EVENTS") == "1"   # overhead check only
+    if not per_launch:
+        ev[0][0].record()
     for k in range(steps):
-        sh.round(0.0, 2**31, events=None if no_events else ev[k])
+        sh.round(0.0, 2**31, events=ev[k] if per_launch else None)
+    if not per_launch:
+        ev[0][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    fused = (el * 1e3 / steps if no_events
-             else sum(a.elapsed_time(b) for a, b in ev) / steps)
+    fused = sum(a.elapsed_time(b) for a, b in ev) / steps
     if world > 1:
         t = torch.tensor([el, fused], dtype=torch.float64,
                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
@@ -186,6 +196,8 @@ def main():
                 "traffic": None if traffic is None else traffic[0],
                 "kernel": "k_round (fused stats + scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
+                "timing": ("HIP events bracketing the K timed launches on the launch stream"
+                           if world == 1 else "HIP events around every timed launch"),
                 "traffic_source": None if traffic is None else traffic[1]}
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
