@@ -630,232 +630,6 @@ k_mfree(const T* a0, const T* __restrict__ s_prev, T* __restrict__ s_next,
 }
 
 // ---------------------------------------------------------------------------
-// wave-granular round kernels (the shipped shape)
-//
-// Same contracts as k_round / k_mfree above, but a row group belongs to ONE
-// wave instead of the whole workgroup: the wave sweeps its R rows' full
-// width (64 lanes x 16 B per access, U accesses in flight per row) and
-// reduces each row sum with a wave64 shuffle tree — no workgroup barrier per
-// group, so a CU never drains its memory pipeline between groups.  Each wave
-// derives m_k / stop_k from its first group's sweep of s (identical in every
-// wave); one barrier at the end combines them for the v update and the state
-// record.  MODE 0: in-place transform (k_round); MODE 1: matrix-free
-// (k_mfree, a read only, v updated over the full vector).
-// ---------------------------------------------------------------------------
-template <typename T, int R, int W, int U, int MODE, int ORDER, bool NT,
-          bool STATS>
-__device__ __forceinline__ void
-wave_group(T* a, const T* __restrict__ s_cur, const T* __restrict__ v_prev,
-           T* __restrict__ s_next, uint32_t rbase, uint32_t ncols,
-           uint32_t row0, bool cyclic, T eps, T& mx, int& ok)
-{
-  using V = typename vec<T, W>::type;
-  const uint32_t nv = ncols / W;
-  const uint32_t lane = threadIdx.x & 63;
-  const V* sv = reinterpret_cast<const V*>(s_cur);
-  const V* vv = reinterpret_cast<const V*>(v_prev);
-  V* rows[R];
-  T inv[R];
-  T acc[R];
-#pragma unroll
-  for (int j = 0; j < R; j++) {
-    rows[j] = reinterpret_cast<V*>(a + (size_t)(rbase + j) * ncols);
-    if constexpr (MODE == 0)
-      inv[j] = (T)1 / s_cur[row0 + rbase + j];
-    acc[j] = (T)0;
-  }
-  auto body = [&](uint32_t c, auto ucount) {
-    constexpr int UU = decltype(ucount)::value;
-    V x[UU][R];
-    V sc[UU];
-#pragma unroll
-    for (int u = 0; u < UU; u++)
-#pragma unroll
-      for (int j = 0; j < R; j++)
-        x[u][j] = ld<V, NT>(rows[j] + c + u * 64);
-#pragma unroll
-    for (int u = 0; u < UU; u++)
-      sc[u] = sv[c + u * 64];
-    if constexpr (STATS) {
-#pragma unroll
-      for (int u = 0; u < UU; u++) {
-        const uint32_t q = c + u * 64;
-        T e[W + 1];
-        if constexpr (W == 1) {
-          e[0] = sc[u];
-        } else {
-#pragma unroll
-          for (int i = 0; i < W; i++)
-            e[i] = sc[u][i];
-        }
-        const uint32_t nxt = (q + 1) * W;
-        const bool has_next = nxt < ncols || cyclic;
-        e[W] = s_cur[nxt < ncols ? nxt : 0];
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-          mx = e[i] > mx ? e[i] : mx;
-          if (i < W - 1 || has_next) {
-            const T d = e[i] - e[i + 1];
-            ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0; // cpp:419-421
-          }
-        }
-      }
-    }
-    if constexpr (MODE == 0) {
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-          if constexpr (ORDER == 0)
-            x[u][j] = x[u][j] * (inv[j] * sc[u]); // cpp:324-325
-          else
-            x[u][j] = (inv[j] * x[u][j]) * sc[u]; // main.py:13-16
-        }
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < R; j++)
-          st<V, NT>(rows[j] + c + u * 64, x[u][j]);
-#pragma unroll
-      for (int u = 0; u < UU; u++)
-#pragma unroll
-        for (int j = 0; j < R; j++)
-          acc[j] += hsum<T, W>(x[u][j]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < UU; u++) {
-        const V xs = vv[c + u * 64] * sc[u];
-#pragma unroll
-        for (int j = 0; j < R; j++) {
-          if constexpr (W == 1) {
-            acc[j] = __builtin_fma(x[u][j], xs, acc[j]);
-          } else {
-#pragma unroll
-            for (int i = 0; i < W; i++)
-              acc[j] = __builtin_fma(x[u][j][i], xs[i], acc[j]);
-          }
-        }
-      }
-    }
-  };
-  uint32_t c = lane;
-  for (; c + (U - 1) * 64 < nv; c += U * 64)
-    body(c, std::integral_constant<int, U>{});
-  if constexpr (U > 1)
-    for (; c < nv; c += 64)
-      body(c, std::integral_constant<int, 1>{});
-#pragma unroll
-  for (int j = 0; j < R; j++) {
-    const T t = wave_sum(acc[j]);
-    if (lane == 0) {
-      if constexpr (MODE == 0) {
-        s_next[rbase + j] = t;
-      } else {
-        const uint32_t r = row0 + rbase + j;
-        s_next[rbase + j] = t / (v_prev[r] * s_cur[r]);
-      }
-    }
-  }
-}
-
-template <typename T, int ROWS, int W, int U, int MODE, int ORDER, bool NT,
-          int BLK = kBlock>
-__global__ __launch_bounds__(BLK) void
-k_round_w(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
-          const T* __restrict__ v_prev, T* __restrict__ v, uint32_t ng_main,
-          uint32_t nrem, uint32_t ncols, uint32_t row0, T eps, uint32_t k,
-          uint32_t max_itr, uint32_t semantics, st_state* state)
-{
-  constexpr int WAVES = BLK / 64;
-  {
-    const uint32_t e =
-      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e != 0 && (MODE == 0 ? e <= k : e < k))
-      return; // an earlier round stopped
-  }
-  __shared__ T mx_sh[WAVES];
-  __shared__ T m_sh;
-  const bool cyclic = semantics == ST_SEM_SYCL;
-  const uint32_t ngroups = ng_main + nrem;
-  const uint32_t gw = blockIdx.x * WAVES + (threadIdx.x >> 6);
-  const uint32_t gstride = gridDim.x * WAVES;
-  T mx = (T)0; // find_max starts from 0 (cpp:185)
-  int ok = 1;
-  T dmx = 0;
-  int dok = 1;
-  for (uint32_t g = gw; g < ngroups; g += gstride) {
-    const bool first = g == gw;
-    if (g < ng_main) {
-      if (first)
-        wave_group<T, ROWS, W, U, MODE, ORDER, NT, true>(
-          a, s_cur, v_prev, s_next, g * ROWS, ncols, row0, cyclic, eps, mx, ok);
-      else
-        wave_group<T, ROWS, W, U, MODE, ORDER, NT, false>(
-          a, s_cur, v_prev, s_next, g * ROWS, ncols, row0, cyclic, eps, dmx,
-          dok);
-    } else {
-      const uint32_t rb = ng_main * ROWS + (g - ng_main);
-      if (first)
-        wave_group<T, 1, W, U, MODE, ORDER, NT, true>(
-          a, s_cur, v_prev, s_next, rb, ncols, row0, cyclic, eps, mx, ok);
-      else
-        wave_group<T, 1, W, U, MODE, ORDER, NT, false>(
-          a, s_cur, v_prev, s_next, rb, ncols, row0, cyclic, eps, dmx, dok);
-    }
-  }
-  // m_k and stop_k: waves without a group contribute the neutral 0 / 1
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0)
-    mx_sh[threadIdx.x >> 6] = mx;
-  const int stop = __syncthreads_and(ok);
-  if (threadIdx.x == 0) {
-    T m = mx_sh[0];
-#pragma unroll
-    for (int w = 1; w < WAVES; w++)
-      m = mx_sh[w] > m ? mx_sh[w] : m;
-    m_sh = m;
-  }
-  __syncthreads();
-  const T m = m_sh;
-  if constexpr (MODE == 0) {
-    // v[r] *= s_k[r] / m_k for this wave's rows (cpp:260)
-    const uint32_t lane = threadIdx.x & 63;
-    for (uint32_t g = gw; g < ngroups; g += gstride) {
-      const uint32_t rb =
-        g < ng_main ? g * ROWS : ng_main * ROWS + (g - ng_main);
-      const uint32_t nr = g < ng_main ? ROWS : 1;
-      if (lane < nr) {
-        const uint32_t r = row0 + rb + lane;
-        v[r] = v[r] * (s_cur[r] / m);
-      }
-    }
-  } else {
-    // v_{k-1} = v_{k-2} * (s_{k-1} / m_{k-1}) over the FULL vector
-    const uint32_t per = (ncols + gridDim.x - 1) / gridDim.x;
-    const uint32_t lo = blockIdx.x * per;
-    const uint32_t hi = lo + per < ncols ? lo + per : ncols;
-    for (uint32_t i = lo + threadIdx.x; i < hi; i += BLK)
-      v[i] = v_prev[i] * (s_cur[i] / m);
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const uint32_t rk = MODE == 0 ? k : k - 1; // the round evaluated
-    state->lambda = (double)s_cur[0]; // cpp:60-65
-    state->max = (double)m;
-    state->stop = stop ? 1u : 0u;
-    state->round = rk;
-    if (stop) {
-      state->iters = semantics == ST_SEM_SYCL ? rk : rk + 1; // cpp:54 / py:47
-      state->end = rk + 1;
-      state->done = 1u;
-    } else if (rk + 1 >= max_itr) { // loop exhausted (cpp:39,54)
-      state->iters = max_itr;
-      state->end = rk + 1;
-      state->done = 1u;
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // round epilogue: one workgroup over the full row-sum vector
 // ---------------------------------------------------------------------------
 template <typename T>

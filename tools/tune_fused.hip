@@ -171,26 +171,6 @@ mfree_variant(Timer& tm, int reps, unsigned grid_cap)
               ROWS, U, (int)NT, BLK, grid, ms, gb);
 }
 
-template <int ROWS, int U, int MODE, int BLK>
-void
-wave_variant(Timer& tm, int reps, unsigned grid_cap)
-{
-  const unsigned ng = g_n / ROWS;
-  const unsigned waves = BLK / 64;
-  const unsigned need = (ng + waves - 1) / waves;
-  const unsigned grid = grid_cap && grid_cap < need ? grid_cap : need;
-  auto f = [&] {
-    hipLaunchKernelGGL((k_round_w<double, ROWS, 2, U, MODE, 0, true, BLK>),
-                       dim3(grid), dim3(BLK), 0, 0, g_a, g_s, g_sn, g_v,
-                       MODE ? g_v2 : g_v, ng, 0u, g_n, 0u, 0.0, 1u, 1u << 30,
-                       0u, g_st);
-  };
-  float ms = tm.run(f, reps);
-  double gb = (MODE ? 1.0 : 2.0) * g_n * (double)g_n * 8 / (ms * 1e-3) / 1e9;
-  std::printf("%s rows=%d u=%d blk=%4d grid=%6u        %8.4f ms  %7.1f GB/s\n",
-              MODE ? "mfreeW" : "roundW", ROWS, U, BLK, grid, ms, gb);
-}
-
 template <int ROWS, int U, int BLK>
 void
 rowsum_variant(Timer& tm, int reps, unsigned grid_cap = 0)
@@ -270,18 +250,6 @@ main(int argc, char** argv)
     ms = tm.run(g, reps);
     std::printf("stream_copy_nt grid=%5u     %8.4f ms  %7.1f GB/s\n", grid, ms,
                 2.0 * nn * 8 / (ms * 1e-3) / 1e9);
-  }
-  for (unsigned cap : { 128u, 256u, 512u, 1024u }) {
-    wave_variant<1, 4, 0, 256>(tm, reps, cap);
-    wave_variant<1, 8, 0, 256>(tm, reps, cap);
-    wave_variant<2, 2, 0, 256>(tm, reps, cap);
-    wave_variant<2, 4, 0, 256>(tm, reps, cap);
-    wave_variant<4, 2, 0, 256>(tm, reps, cap);
-    wave_variant<2, 4, 0, 512>(tm, reps, cap);
-    wave_variant<1, 8, 1, 256>(tm, reps, cap);
-    wave_variant<2, 4, 1, 256>(tm, reps, cap);
-    wave_variant<4, 2, 1, 256>(tm, reps, cap);
-    wave_variant<4, 4, 1, 256>(tm, reps, cap);
   }
   round_variant<2, 2, true, 256>(tm, reps, 256);
   mfree_variant<4, 2, true, 256>(tm, reps, 512);
