@@ -532,6 +532,40 @@ def test_error_paths_and_degenerate_inputs(eigen):
     assert itr == 6 and st["converged"] == 0 and np.isnan(lam)
 
 
+def _rccl_worker(rank, port, outdir):
+    import torch.distributed as dist
+    from eigen_value_amd.sharded import ShardedSimilarityTransform, _allgather
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        # the in-slot all-gather the sharded loop issues every round, on RCCL
+        out = torch.arange(12, dtype=torch.float64, device="cuda")
+        _allgather(out, out[0:12])
+        assert torch.equal(out, torch.arange(12, dtype=torch.float64, device="cuda"))
+        sh = ShardedSimilarityTransform(2048, torch.float64)
+        sh.load("hilbert")
+        lam, v, iters, rounds = sh.solve()
+        np.save(os.path.join(outdir, "rccl.npy"), np.array([lam, iters, rounds]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_process_group_single_rank(tmp_path, orc):
+    """P = 1 over the nccl (= RCCL) backend: the sharded driver under an
+    initialised RCCL process group, and the in-place all-gather call."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_rccl_worker, args=(port, str(tmp_path)), nprocs=1, join=True)
+    lam, iters, rounds = np.load(tmp_path / "rccl.npy")
+    ref = orc.similarity_transform(orc.hilbert(2048), orc.SEM_SYCL)
+    assert int(iters) == ref.iter_count == 14
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess
