@@ -5,7 +5,8 @@ ARCH     ?= gfx950
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fno-fast-math -Wall -Wextra -Wno-unused-parameter -Iinclude \
             -Ieigen_value_amd/csrc
-SRC      := eigen_value_amd/csrc/st_kernels.hip eigen_value_amd/csrc/st_solve.hip
+SRC      := eigen_value_amd/csrc/st_kernels.hip eigen_value_amd/csrc/st_solve.hip \
+            eigen_value_amd/csrc/st_multi.hip
 OBJ      := $(patsubst eigen_value_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB      := eigen_value_amd/lib/libsimilarity_transform.so
 
@@ -17,7 +18,7 @@ build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value
 
 $(LIB): $(OBJ)
 	@mkdir -p eigen_value_amd/lib
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

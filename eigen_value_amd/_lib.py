@@ -116,6 +116,9 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_use_own_stream.argtypes = [P]
     L.st_use_own_stream.restype = i32
     for sfx, T in (("f32", f32), ("f64", f64)):
+        fm = getattr(L, f"st_solve_multi_{sfx}")
+        fm.argtypes = [P, u32, i32, P, i32, u64, P, P, P, P, P]
+        fm.restype = i64
         fn = getattr(L, f"st_solve_device_{sfx}")
         fn.argtypes = [P, P, u32, P, P, P, P, P, P]
         fn.restype = i64

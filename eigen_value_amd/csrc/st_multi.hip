@@ -1,0 +1,327 @@
+// st_multi.hip — native multi-GPU solve: one process, P devices, row-block
+// sharding with ONE RCCL all-gather of the N-length row-sum vector per round
+// (SURVEY.md §8e), driven from one host thread with ncclGroupStart/End.
+//
+// Device d owns rows [d*chunk, d*chunk + rows_d), chunk = ceil(N/P), and
+// keeps: its row block of A (transformed in place, or read only in the
+// matrix-free form), two padded P*chunk row-sum vectors (ping-pong), the
+// eigenvector accumulator(s) and an st_state.  Round k on every device:
+//   k_round  (or k_mfree, launch k+1) on its stream      st_device.h
+//   ncclAllGather(slot_d, s_next, chunk, type, comm_d, stream_d)
+// Every device derives m_k / stop_k from the identical gathered vector, so
+// the states agree without a further collective; the host polls device 0's
+// flag per batch, as in the single-GPU loop (st_solve.hip).  At the end the
+// eigenvector rows come back from each device's own slice (transform form)
+// or from device 0's full copy (matrix-free form).
+//
+// This is the C-ABI counterpart of eigen_value_amd/sharded.py (one process
+// per GPU over torch.distributed); both run the same kernels.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cstring>
+#include <vector>
+
+#include "st_internal.h"
+
+namespace st {
+namespace {
+
+#define ST_NCCL(expr)                                                          \
+  do {                                                                         \
+    ncclResult_t r_ = (expr);                                                  \
+    if (r_ != ncclSuccess) {                                                   \
+      ::st::set_error("%s:%d: %s failed: %s", __FILE__, __LINE__, #expr,       \
+                      ncclGetErrorString(r_));                                 \
+      return -1;                                                               \
+    }                                                                          \
+  } while (0)
+
+template <typename T>
+ncclDataType_t
+nccl_type();
+template <>
+ncclDataType_t
+nccl_type<float>()
+{
+  return ncclFloat;
+}
+template <>
+ncclDataType_t
+nccl_type<double>()
+{
+  return ncclDouble;
+}
+
+template <typename T>
+struct Shard
+{
+  int dev = 0;
+  uint32_t row0 = 0, nrows = 0;
+  hipStream_t stream = nullptr;
+  ncclComm_t comm = nullptr;
+  T* a = nullptr;
+  T* s[2] = { nullptr, nullptr };
+  T* v[2] = { nullptr, nullptr };
+  st_state* state = nullptr;
+};
+
+template <typename T>
+struct Multi
+{
+  std::vector<Shard<T>> sh;
+  st_state* h_state = nullptr; // pinned, 2 slots
+  hipEvent_t ev[2] = { nullptr, nullptr };
+  ~Multi()
+  {
+    for (auto& d : sh) {
+      (void)hipSetDevice(d.dev);
+      if (d.stream)
+        (void)hipStreamSynchronize(d.stream);
+      if (d.comm)
+        (void)ncclCommDestroy(d.comm);
+      (void)hipFree(d.a);
+      for (int i = 0; i < 2; i++) {
+        (void)hipFree(d.s[i]);
+        (void)hipFree(d.v[i]);
+      }
+      (void)hipFree(d.state);
+      if (d.stream)
+        (void)hipStreamDestroy(d.stream);
+    }
+    if (!sh.empty())
+      (void)hipSetDevice(sh[0].dev);
+    for (hipEvent_t e : ev)
+      if (e)
+        (void)hipEventDestroy(e);
+    if (h_state)
+      (void)hipHostFree(h_state);
+  }
+};
+
+template <typename T>
+int
+gather(Multi<T>& M, int which, uint32_t chunk)
+{
+  // P = 1 still issues the (in-place, no-op) collective, so the RCCL path
+  // is exercised on a one-GPU machine too
+  ST_NCCL(ncclGroupStart());
+  for (size_t p = 0; p < M.sh.size(); p++) {
+    Shard<T>& d = M.sh[p];
+    T* buf = d.s[which];
+    ST_NCCL(ncclAllGather(buf + p * chunk, buf, chunk, nccl_type<T>(), d.comm,
+                          d.stream));
+  }
+  ST_NCCL(ncclGroupEnd());
+  return 0;
+}
+
+template <typename T>
+int64_t
+solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
+            int gen_kind, uint64_t seed, T* eigen_val, T* eigen_vec,
+            uint32_t* iter_cnt, const st_options* opt, st_stats* stats)
+{
+  ST_REQUIRE(n > 0, "dim must be > 0");
+  ST_REQUIRE(ngpus >= 1, "ngpus must be >= 1");
+  ST_REQUIRE(eigen_val && eigen_vec && iter_cnt, "null output pointer");
+  ST_REQUIRE(gen_kind >= 0 && gen_kind <= 2, "gen_kind must be 0, 1 or 2");
+  ST_REQUIRE(gen_kind != 0 || mat, "null matrix");
+  int have = 0;
+  ST_CHECK(hipGetDeviceCount(&have));
+  const uint32_t P = (uint32_t)ngpus;
+  const uint32_t chunk = (n + P - 1) / P;
+  ST_REQUIRE((uint64_t)(P - 1) * chunk < n,
+             "dim %u leaves a device of %u without rows", n, P);
+  const double eps_d = (opt && opt->eps >= 0.0)
+                         ? opt->eps
+                         : (sizeof(T) == 4 ? (double)ST_EPS_F32 : ST_EPS_F64);
+  const T eps = (T)eps_d;
+  const uint32_t max_itr = (opt && opt->max_itr) ? opt->max_itr : ST_MAX_ITR;
+  const uint32_t sem = opt ? opt->semantics : ST_SEM_SYCL;
+  const uint32_t batch = (opt && opt->batch) ? opt->batch : 8u;
+  const bool mfree = opt && (opt->flags & ST_FLAG_MATRIX_FREE);
+  ST_REQUIRE(sem <= ST_SEM_MAINPY, "unknown semantics %u", sem);
+
+  Multi<T> M;
+  M.sh.resize(P);
+  std::vector<int> devlist(P);
+  for (uint32_t p = 0; p < P; p++) {
+    devlist[p] = devices ? devices[p] : (int)p;
+    ST_REQUIRE(devlist[p] >= 0 && devlist[p] < have,
+               "device %d out of range (%d devices)", devlist[p], have);
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t p = 0; p < P; p++) {
+    Shard<T>& d = M.sh[p];
+    d.dev = devlist[p];
+    d.row0 = p * chunk;
+    d.nrows = (d.row0 + chunk <= n) ? chunk : n - d.row0;
+    ST_CHECK(hipSetDevice(d.dev));
+    ST_CHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+    ST_CHECK(hipMalloc(&d.a, sizeof(T) * (size_t)d.nrows * n));
+    for (int i = 0; i < 2; i++)
+      ST_CHECK(hipMalloc(&d.s[i], sizeof(T) * (size_t)P * chunk));
+    for (int i = 0; i < (mfree ? 2 : 1); i++)
+      ST_CHECK(hipMalloc(&d.v[i], sizeof(T) * (size_t)P * chunk));
+    ST_CHECK(hipMalloc(&d.state, sizeof(st_state)));
+    ST_CHECK(hipMemsetAsync(d.state, 0, sizeof(st_state), d.stream));
+    if (gen_kind == 0) {
+      ST_CHECK(hipMemcpyAsync(d.a, mat + (size_t)d.row0 * n,
+                              sizeof(T) * (size_t)d.nrows * n,
+                              hipMemcpyHostToDevice, d.stream));
+    } else if (gen_kind == 1) {
+      if (sizeof(T) == 8)
+        ST_REQUIRE(st_generate_hilbert_f64((double*)d.a, d.nrows, n, d.row0,
+                                           d.stream) == 0,
+                   "%s", eigen_last_error());
+      else
+        ST_REQUIRE(st_generate_hilbert_f32((float*)d.a, d.nrows, n, d.row0,
+                                           d.stream) == 0,
+                   "%s", eigen_last_error());
+    } else {
+      if (sizeof(T) == 8)
+        ST_REQUIRE(st_generate_random_f64((double*)d.a, d.nrows, n, d.row0,
+                                          seed, d.stream) == 0,
+                   "%s", eigen_last_error());
+      else
+        ST_REQUIRE(st_generate_random_f32((float*)d.a, d.nrows, n, d.row0,
+                                          seed, d.stream) == 0,
+                   "%s", eigen_last_error());
+    }
+    if (launch_fill<T>(d.v[0], n, (T)1, d.stream)) // cpp:34
+      return -1;
+  }
+  ST_CHECK(hipSetDevice(M.sh[0].dev));
+  ST_CHECK(hipHostMalloc(&M.h_state, 2 * sizeof(st_state), hipHostMallocDefault));
+  ST_CHECK(hipEventCreateWithFlags(&M.ev[0], hipEventDisableTiming));
+  ST_CHECK(hipEventCreateWithFlags(&M.ev[1], hipEventDisableTiming));
+  {
+    std::vector<ncclComm_t> comms(P);
+    ST_NCCL(ncclCommInitAll(comms.data(), (int)P, devlist.data()));
+    for (uint32_t p = 0; p < P; p++)
+      M.sh[p].comm = comms[p];
+  }
+  for (uint32_t p = 0; p < P; p++) { // s_0 = rowsum(A_0), then gather
+    Shard<T>& d = M.sh[p];
+    ST_CHECK(hipSetDevice(d.dev));
+    if (launch_rowsum<T>(d.a, d.s[0] + p * chunk, d.nrows, n, d.stream))
+      return -1;
+  }
+  if (gather(M, 0, chunk))
+    return -1;
+  for (uint32_t p = 0; p < P; p++) { // the setup is not part of the loop time
+    ST_CHECK(hipSetDevice(M.sh[p].dev));
+    ST_CHECK(hipStreamSynchronize(M.sh[p].stream));
+  }
+  const double setup_ms =
+    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                              t0)
+      .count();
+
+  const auto t1 = std::chrono::steady_clock::now();
+  uint32_t enqueued = 0, cur = 0, batch_no = 0;
+  bool done = false;
+  while (!done && enqueued < max_itr) {
+    const uint32_t b = (max_itr - enqueued) < batch ? (max_itr - enqueued) : batch;
+    for (uint32_t j = 0; j < b; j++) {
+      const uint32_t k = enqueued + j;
+      for (uint32_t p = 0; p < P; p++) {
+        Shard<T>& d = M.sh[p];
+        ST_CHECK(hipSetDevice(d.dev));
+        int rc;
+        if (mfree)
+          rc = launch_mfree<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk,
+                               d.v[k & 1], d.v[(k + 1) & 1], d.nrows, n,
+                               d.row0, eps, k + 1, max_itr, sem, d.state,
+                               d.stream);
+        else
+          rc = launch_round<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk, d.v[0],
+                               d.nrows, n, d.row0, eps, k, max_itr, sem,
+                               d.state, d.stream);
+        if (rc)
+          return -1;
+      }
+      if (gather(M, cur ^ 1, chunk))
+        return -1;
+      cur ^= 1;
+    }
+    enqueued += b;
+    const int slot = batch_no & 1;
+    Shard<T>& d0 = M.sh[0];
+    ST_CHECK(hipSetDevice(d0.dev));
+    ST_CHECK(hipMemcpyAsync(&M.h_state[slot], d0.state, sizeof(st_state),
+                            hipMemcpyDeviceToHost, d0.stream));
+    ST_CHECK(hipEventRecord(M.ev[slot], d0.stream));
+    if (batch_no > 0) {
+      ST_CHECK(hipEventSynchronize(M.ev[slot ^ 1]));
+      done = M.h_state[slot ^ 1].done != 0;
+    }
+    batch_no++;
+  }
+  for (uint32_t p = 0; p < P; p++) {
+    ST_CHECK(hipSetDevice(M.sh[p].dev));
+    ST_CHECK(hipStreamSynchronize(M.sh[p].stream));
+  }
+  const double loop_ms =
+    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                              t1)
+      .count();
+  st_state fin;
+  ST_CHECK(hipSetDevice(M.sh[0].dev));
+  ST_CHECK(hipMemcpy(&fin, M.sh[0].state, sizeof(st_state), hipMemcpyDeviceToHost));
+  ST_REQUIRE(fin.done, "internal: loop ended without done flag");
+  *eigen_val = (T)fin.lambda;
+  *iter_cnt = fin.iters;
+  if (mfree) {
+    ST_CHECK(hipMemcpy(eigen_vec, M.sh[0].v[fin.end & 1u], sizeof(T) * (size_t)n,
+                       hipMemcpyDeviceToHost));
+  } else {
+    for (uint32_t p = 0; p < P; p++) {
+      Shard<T>& d = M.sh[p];
+      ST_CHECK(hipSetDevice(d.dev));
+      ST_CHECK(hipMemcpy(eigen_vec + d.row0, d.v[0] + d.row0,
+                         sizeof(T) * (size_t)d.nrows, hipMemcpyDeviceToHost));
+    }
+  }
+  if (stats) {
+    std::memset(stats, 0, sizeof(*stats));
+    stats->h2d_ms = setup_ms;
+    stats->loop_ms = loop_ms;
+    stats->rounds = fin.end;
+    stats->converged = fin.stop;
+  }
+  return (int64_t)(setup_ms + loop_ms);
+}
+
+} // namespace
+} // namespace st
+
+extern "C" {
+
+int64_t
+st_solve_multi_f32(const float* mat, unsigned int dim, int ngpus,
+                   const int* devices, int gen_kind, uint64_t seed,
+                   float* eigen_val, float* eigen_vec, unsigned int* iter_cnt,
+                   const st_options* opt, st_stats* stats)
+{
+  st::clear_error();
+  return st::solve_multi<float>(mat, dim, ngpus, devices, gen_kind, seed,
+                                eigen_val, eigen_vec, iter_cnt, opt, stats);
+}
+
+int64_t
+st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
+                   const int* devices, int gen_kind, uint64_t seed,
+                   double* eigen_val, double* eigen_vec,
+                   unsigned int* iter_cnt, const st_options* opt,
+                   st_stats* stats)
+{
+  st::clear_error();
+  return st::solve_multi<double>(mat, dim, ngpus, devices, gen_kind, seed,
+                                 eigen_val, eigen_vec, iter_cnt, opt, stats);
+}
+
+} // extern "C"

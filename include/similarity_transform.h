@@ -137,6 +137,29 @@ int64_t st_solve_device_f64(void* wq, double* d_mat, unsigned int dim,
                             const st_options* opt, st_stats* stats);
 
 /* ---------------------------------------------------------------------- */
+/* 3b. native multi-GPU solve (one process, ngpus devices, RCCL)           */
+/* ---------------------------------------------------------------------- */
+
+/* Row-block sharded solve over `ngpus` devices (`devices` = list of HIP
+ * device ids, or NULL for 0..ngpus-1) with ONE ncclAllGather of the row-sum
+ * vector per round.  Input: gen_kind 0 = host matrix `mat`
+ * (dim x dim, row-major; each device copies its rows), 1 = Hilbert,
+ * 2 = seeded random (generated on each device for its rows; `mat` unused).
+ * Outputs on the host.  opt may select ST_FLAG_MATRIX_FREE.  stats->h2d_ms
+ * reports the setup (allocation, input, communicator, first row sums),
+ * stats->loop_ms the round loop.  Returns total ms or negative. */
+int64_t st_solve_multi_f32(const float* mat, unsigned int dim, int ngpus,
+                           const int* devices, int gen_kind, uint64_t seed,
+                           float* eigen_val, float* eigen_vec,
+                           unsigned int* iter_cnt, const st_options* opt,
+                           st_stats* stats);
+int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
+                           const int* devices, int gen_kind, uint64_t seed,
+                           double* eigen_val, double* eigen_vec,
+                           unsigned int* iter_cnt, const st_options* opt,
+                           st_stats* stats);
+
+/* ---------------------------------------------------------------------- */
 /* 4. step-level kernels (asynchronous on `stream`, a hipStream_t or NULL) */
 /* ---------------------------------------------------------------------- */
 

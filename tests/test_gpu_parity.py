@@ -566,6 +566,26 @@ def test_rccl_process_group_single_rank(tmp_path, orc):
     assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
 
 
+@pytest.mark.parametrize("matrix_free", [False, True])
+def test_native_multi_gpu_solve(orc, matrix_free):
+    """st_solve_multi_* (one process, RCCL communicator over the visible
+    devices; P = 1 here, the all-gather still issued) vs the oracle."""
+    from eigen_value_amd.multi import solve_multi
+    ngpu = torch.cuda.device_count()
+    n = 3001
+    lam, v, it, st = solve_multi(n, "random", ngpus=ngpu, seed=3, matrix_free=matrix_free)
+    ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL)
+    assert it == ref.iter_count and st["rounds"] == ref.rounds_evaluated
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
+    # host-matrix input, fp32 Hilbert: the reference's published 9 rounds
+    mat = orc.hilbert(128, np.float32)
+    lam32, v32, it32, _ = solve_multi(128, mat, ngpus=ngpu, matrix_free=matrix_free)
+    assert it32 == 9 and abs(lam32 - 2.2171896) < 1e-5
+    with pytest.raises(_lib.EigenValueError, match="without rows"):
+        solve_multi(1, "hilbert", devices=[0, 0])
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess
