@@ -378,8 +378,16 @@ def test_full_size_properties(solver):
     a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
     lam, v, itr, _ = solver.solve(a, inplace=True)
     dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
-    r = torch.mv(a, v) - lam * v                       # torch fp64 as the checker only
+    av = torch.mv(a, v)                                # torch fp64 as the checker only
+    r = av - lam * v
     assert (r.abs().max() / (lam * v.abs().max())).item() < 1e-9
+    # Collatz–Wielandt: for a positive matrix and v > 0 the true Perron root
+    # lies in [min (Av)_i/v_i, max (Av)_i/v_i]; the bracket proves the
+    # north star's "within 1e-6 rel. of the true eigenvalue" at full size
+    q = av / v
+    lo, hi = q.min().item(), q.max().item()
+    assert v.min().item() > 0 and lo <= lam * (1 + 1e-12) and hi >= lam * (1 - 1e-12)
+    assert (hi - lo) / lam < 1e-6
     # homogeneity over a fixed number of rounds: every quantity of the
     # iteration on 2A is exactly twice (s, λ) or equal to (v, D^-1 A D
     # ratios) that on A, bit for bit
