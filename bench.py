@@ -96,6 +96,14 @@ def load_traffic(workload: str, kernel: str = "k_round"):
     return best
 
 
+def cw_width(torch, a0, v):
+    """(max - min) / mid of (A0 v)_i / v_i: the relative width of the
+    Collatz–Wielandt bracket that contains the true Perron root."""
+    q = torch.mv(a0, v.to(a0.dtype)) / v.to(a0.dtype)
+    lo, hi = q.min().item(), q.max().item()
+    return (hi - lo) / (0.5 * (hi + lo))
+
+
 def timed_rounds(sh, steps, warmup, torch, dist, world):
     """Warmup + K timed rounds; returns (elapsed_s_max, kernel_ms_avg).
 
@@ -182,6 +190,17 @@ def main():
         solve["check"] = {"iter_count_expected": HILBERT8192_F64[0],
                           "eigen_val_rel_err_vs_oracle":
                               abs(lam - HILBERT8192_F64[1]) / HILBERT8192_F64[1]}
+    if world == 1:
+        # accuracy against the TRUE eigenvalue: Collatz–Wielandt bracket of the
+        # positive input, min (A0 v)_i / v_i <= λ_true <= max (A0 v)_i / v_i
+        # (torch.mv as the checker); and the same solve at eps = 1e-6
+        a0 = sh.load(args.kind)
+        solve["cw_bracket_rel_width"] = cw_width(torch, a0, v)
+        lam6, v6, it6, _ = sh.solve(eps=1e-6, max_itr=1000, batch=1)
+        a0 = sh.load(args.kind)
+        solve["eps_1e-6"] = {"iter_count": it6, "eigen_val": lam6,
+                             "cw_bracket_rel_width": cw_width(torch, a0, v6)}
+        del a0
 
     # ---- timed rounds ----------------------------------------------------
     sh.load(args.kind, mat=None)
