@@ -96,12 +96,12 @@ def load_traffic(workload: str, kernel: str = "k_round"):
     return best
 
 
-def cw_width(torch, a0, v):
-    """(max - min) / mid of (A0 v)_i / v_i: the relative width of the
-    Collatz–Wielandt bracket that contains the true Perron root."""
+def cw_bound(torch, a0, v, lam):
+    """Bound on |λ - λ_true| / λ from the Collatz–Wielandt bracket of a
+    positive matrix: λ_true lies in [min, max] of (A0 v)_i / v_i."""
     q = torch.mv(a0, v.to(a0.dtype)) / v.to(a0.dtype)
     lo, hi = q.min().item(), q.max().item()
-    return (hi - lo) / (0.5 * (hi + lo))
+    return max(abs(lam - lo), abs(lam - hi)) / abs(lam)
 
 
 def timed_rounds(sh, steps, warmup, torch, dist, world):
@@ -195,11 +195,11 @@ def main():
         # positive input, min (A0 v)_i / v_i <= λ_true <= max (A0 v)_i / v_i
         # (torch.mv as the checker); and the same solve at eps = 1e-6
         a0 = sh.load(args.kind)
-        solve["cw_bracket_rel_width"] = cw_width(torch, a0, v)
+        solve["rel_err_bound_vs_true"] = cw_bound(torch, a0, v, lam)
         lam6, v6, it6, _ = sh.solve(eps=1e-6, max_itr=1000, batch=1)
         a0 = sh.load(args.kind)
         solve["eps_1e-6"] = {"iter_count": it6, "eigen_val": lam6,
-                             "cw_bracket_rel_width": cw_width(torch, a0, v6)}
+                             "rel_err_bound_vs_true": cw_bound(torch, a0, v6, lam6)}
         del a0
 
     # ---- timed rounds ----------------------------------------------------
