@@ -128,7 +128,7 @@ def scale_rowsum(mat, s_cur, s_next=None, row0: int = 0,
         _ptr(state), _stream(mat.device)), "scale_rowsum")
 
 
-def round(mat, s_cur, s_next, v, state, row0: int = 0, eps: float = 1e-3, k: int = 0,
+def fused_round(mat, s_cur, s_next, v, state, row0: int = 0, eps: float = 1e-3, k: int = 0,
           max_itr: int = _lib.ST_MAX_ITR, semantics: int = _lib.ST_SEM_SYCL) -> None:
     """One whole round k in one launch (``st_round_*``): stats of the full
     s_cur, v update of the local rows, in-place transform, s_next."""

@@ -86,7 +86,7 @@ class HipShardOps:
         self.dev.epilogue(s, v, state, eps, max_itr, semantics)
 
     def round(self, mat, s_cur, s_next, v, row0, eps, k, max_itr, semantics, state):
-        self.dev.round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
+        self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
                        max_itr=max_itr, semantics=semantics, state=state)
 
     def mfree_round(self, mat0, s_prev, s_next, v_prev, v_cur, row0, eps, k, max_itr,

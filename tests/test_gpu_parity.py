@@ -141,7 +141,7 @@ def test_round_kernel_vs_oracle(orc, dt, sem, nrows, ncols, row0):
     state = dev.new_state(DEV)
     if row0 + nrows > ncols:
         pytest.skip("row block must lie inside the s vector")
-    dev.round(ta, ts, s_next, tv, state, row0=row0, eps=1e-3, k=0, semantics=sem)
+    dev.fused_round(ta, ts, s_next, tv, state, row0=row0, eps=1e-3, k=0, semantics=sem)
     order = 0 if sem == _lib.ST_SEM_SYCL else 1
     ref = orc.compute_next(a, s_full, row0=row0, order=order)
     assert np.array_equal(to_np(ta), ref)
@@ -166,17 +166,17 @@ def test_round_stop_and_gating(orc):
     s_next = torch.empty_like(s)
     v = torch.ones_like(s)
     state = dev.new_state(DEV)
-    dev.round(a, s, s_next, v, state, k=0)
+    dev.fused_round(a, s, s_next, v, state, k=0)
     st = dev.read_state(state)
     assert st["stop"] == 1 and st["done"] == 1 and st["end"] == 1 and st["iters"] == 0
     after = a.clone()
     assert torch.equal(after, keep)           # D^-1 A D with constant s is the identity map
-    dev.round(a, s * 2.0, s_next, v, state, k=1)    # a later round: no-op
+    dev.fused_round(a, s * 2.0, s_next, v, state, k=1)    # a later round: no-op
     assert torch.equal(a, after) and dev.read_state(state)["end"] == 1
     # max_itr exhaustion on round k = max_itr - 1
     state2 = dev.new_state(DEV)
     s2 = torch.from_numpy(orc.random_matrix(n, 2, nrows=1)[0] + 1.0).to(DEV)
-    dev.round(a, s2, s_next, v, state2, k=4, max_itr=5)
+    dev.fused_round(a, s2, s_next, v, state2, k=4, max_itr=5)
     st2 = dev.read_state(state2)
     assert st2["done"] == 1 and st2["stop"] == 0 and st2["iters"] == 5 and st2["end"] == 5
 
