@@ -258,11 +258,11 @@ def main():
         ns.load("random", seed=0)
         lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=1)
         ns.load("random", seed=0)
-        el_ns, fused_ns = timed_rounds(ns, 20, 3, torch, dist, 1)
+        el_ns, fused_ns = timed_rounds(ns, 50, 3, torch, dist, 1)
         by = 2.0 * 32768 * 32768 * 8
         ach = by / (fused_ns * 1e-3) / 1e9
         tr = load_traffic("random32768_f64")
-        out["north_star"] = {"workload": "random32768_f64", "ms_per_iteration": round(el_ns / 20 * 1e3, 4),
+        out["north_star"] = {"workload": "random32768_f64", "ms_per_iteration": round(el_ns / 50 * 1e3, 4),
                              "fused_ms_avg": round(fused_ns, 4), "achieved": round(ach, 1),
                              "frac": round(ach / HBM_PEAK_GBS, 4), "target_frac": 0.70,
                              "traffic": None if tr is None else tr[0],
@@ -273,12 +273,12 @@ def main():
         mf = sharded.ShardedSimilarityTransform(32768, torch.float64, matrix_free=True)
         mf.load("random", seed=0)
         lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=1)
-        el_mf, k_mf = timed_rounds(mf, 20, 3, torch, dist, 1)
+        el_mf, k_mf = timed_rounds(mf, 50, 3, torch, dist, 1)
         by_mf = 1.0 * 32768 * 32768 * 8
         tr_mf = load_traffic("random32768_f64", "k_mfree")
         out["north_star"]["matrix_free"] = {
             "traffic": None if tr_mf is None else tr_mf[0],
-            "ms_per_iteration": round(el_mf / 20 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
+            "ms_per_iteration": round(el_mf / 50 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
             "achieved": round(by_mf / (k_mf * 1e-3) / 1e9, 1),
             "frac": round(by_mf / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
             "bytes_per_round": by_mf, "solve_iter_count": it_mf,

@@ -92,3 +92,33 @@ def test_header_compiles_as_c_and_cxx(tmp_path):
                       '  return f ? (int)sizeof(st_options)-24 : 1; }\n')
     subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", f"-I{inc}", "-c", str(src_cc),
                     "-o", str(tmp_path / "tcc.o")], check=True)
+
+
+def test_wrapper_argument_checks_match_reference():
+    # wrapper/python/similarity_transform.py:55-57: square, float32 asserted
+    # before any library call (float64 is additionally accepted here)
+    from eigen_value_amd.similarity_transform import EigenValue
+    ev = object.__new__(EigenValue)          # no device needed for the checks
+    with pytest.raises(AssertionError, match="square"):
+        ev.similarity_transform(np.ones((3, 4), np.float32))
+    with pytest.raises(AssertionError, match="float32"):
+        ev.similarity_transform(np.ones((3, 3), np.int64))
+    with pytest.raises(TypeError):
+        ev.similarity_transform_ex(np.ones((3, 3), np.float16))
+
+
+def test_sharded_partition_rejects_empty_rank():
+    torch = pytest.importorskip("torch")
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+
+    class Dummy:
+        def empty(self, shape, dtype):
+            return torch.zeros(shape, dtype=dtype)
+
+        def new_state(self):
+            return {}
+
+    import torch.distributed as dist
+    assert not dist.is_initialized()
+    sh = ShardedSimilarityTransform(5, torch.float64, ops=Dummy())   # world 1
+    assert (sh.part.row0, sh.part.nrows, sh.part.chunk) == (0, 5, 5)
