@@ -594,6 +594,36 @@ def test_native_multi_gpu_solve(orc, matrix_free):
         solve_multi(1, "hilbert", devices=[0, 0])
 
 
+def test_fuzz_vs_oracle(eigen, orc):
+    """Seeded random sweep over size, dtype, semantics, form, batch and
+    eps: iteration counts equal to the oracle's, λ / v within the dtype's
+    tolerance.  Sizes straddle the launch-shape switches (rows per group,
+    remainder groups, 16-byte vs element access)."""
+    rng = np.random.default_rng(1234)
+    for case in range(40):
+        n = int(rng.choice([1, 2, 3, 7, 64, 127, 255, 1023, 1024, 1025, 2047, 2048, 2049,
+                            2051, 3000]))
+        dt = np.float64 if rng.random() < 0.6 else np.float32
+        sem = int(rng.integers(0, 2))
+        mf = bool(rng.random() < 0.4)
+        batch = int(rng.choice([1, 2, 5, 8, 16]))
+        eps = float(rng.choice([1e-3, 1e-6, 1e-2]))
+        kind = "hilbert" if rng.random() < 0.5 else "random"
+        mat = orc.hilbert(n, dt) if kind == "hilbert" else orc.random_matrix(n, case, dt)
+        lam, v, ts, itr, st = eigen.similarity_transform_ex(
+            mat, eps=eps, semantics=sem, matrix_free=mf, batch=batch, max_itr=200)
+        ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=200)
+        tag = (case, n, dt.__name__, sem, mf, batch, eps, kind)
+        # a stop test within rounding of eps can legitimately flip in fp32
+        dmin = np.min(np.abs(ref.max_dsum - eps)) if len(ref.max_dsum) else 1.0
+        if dt == np.float32 and dmin < 1e-5 * max(1.0, float(np.max(mat.sum(1)))):
+            continue
+        assert itr == ref.iter_count, tag
+        tol = 1e-10 if dt == np.float64 else 2e-5
+        assert abs(lam - ref.eigen_val) <= tol * abs(ref.eigen_val) + 1e-30, tag
+        assert np.max(np.abs(v - ref.eigen_vec)) <= (1e-10 if dt == np.float64 else 5e-4), tag
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess
