@@ -42,10 +42,12 @@ check_launch(const char* what)
 // profiles/r01_tuning.md).  The in-place read+write stream peaks with few
 // streams in flight: 2 rows per group, 2 column chunks of 16 B per lane per
 // row, non-temporal matrix loads/stores, one 256-thread workgroup per CU
-// striding over the row groups for matrices >= 1 GiB (2 per CU below).
+// striding over the row groups (4 rows per group below 1 GiB, where rows
+// are short; 1 row and 2 workgroups per CU below 1024 rows).
 // The read-only matrix-free sweep peaks with 4 rows per group, 2 chunks in
 // flight, 2 workgroups per CU for matrices >= 1 GiB (4 per CU below).
-constexpr int kRows = 2;
+constexpr int kRows = 2;      // matrices >= 1 GiB
+constexpr int kRowsShort = 4; // below: 4 rows share each group's reduction
 constexpr int kUnroll = 2;
 constexpr bool kNontemporal = true;
 constexpr uint32_t kGridCap = 512;
@@ -62,7 +64,10 @@ mfree_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
 inline uint32_t
 round_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  return (size_t)nrows * ncols * elem >= ((size_t)1 << 30) ? 256u : 512u;
+  // one workgroup per CU once the rows are grouped (>= 1024 rows), else two
+  (void)ncols;
+  (void)elem;
+  return nrows >= 2 * kGridCap ? 256u : 512u;
 }
 
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER>
@@ -139,9 +144,14 @@ launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                   uint32_t max_itr, uint32_t semantics, st_state* st,
                   hipStream_t stream)
 {
-  if (nrows < 2 * kGridCap)
+  const size_t bytes = (size_t)nrows * ncols * sizeof(T);
+  if (nrows < 2 * kGridCap) // small: one row per group keeps the CUs busy
     launch_round_cfg<T, 1, W, ORDER>(a, s_cur, s_next, v, nrows, ncols, row0,
                                      eps, k, max_itr, semantics, st, stream);
+  else if (bytes < ((size_t)1 << 30)) // short rows: amortise the per-group
+    launch_round_cfg<T, kRowsShort, W, ORDER>(a, s_cur, s_next, v, nrows,
+                                              ncols, row0, eps, k, max_itr,
+                                              semantics, st, stream);
   else
     launch_round_cfg<T, kRows, W, ORDER>(a, s_cur, s_next, v, nrows, ncols,
                                          row0, eps, k, max_itr, semantics, st,
