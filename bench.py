@@ -286,6 +286,28 @@ def main():
         del mf
         torch.cuda.empty_cache()
 
+    # ---- the reference's own headline, apples to apples ----------------
+    # README.md:66-158 of the reference publishes whole solves of the fp32
+    # 8192x8192 Hilbert matrix through its C++ entry (host matrix in, H2D
+    # inside the timed region); the fastest published device is a Xeon
+    # Platinum 8358 at 126 ms (17 rounds).  Same call shape here: the
+    # drop-in max_eigen_value on a host fp32 Hilbert matrix.
+    if world == 1 and rank == 0:
+        from eigen_value_amd.similarity_transform import EigenValue
+        idx = np.arange(8192, dtype=np.int64)
+        h32 = np.float32(1.0) / (idx[:, None] + idx[None, :] + 1).astype(np.float32)  # utils.cpp:150
+        with EigenValue() as e:
+            e.similarity_transform(h32)                      # warm the context
+            runs = [e.similarity_transform_ex(h32) for _ in range(3)]
+        lam32, _, ts32, it32, st32 = min(runs, key=lambda r: r[4]["h2d_ms"] + r[4]["loop_ms"])
+        out["reference_headline"] = {
+            "workload": "hilbert8192_f32 whole solve via max_eigen_value (host matrix)",
+            "ms": round(st32["h2d_ms"] + st32["loop_ms"], 3), "h2d_ms": round(st32["h2d_ms"], 3),
+            "loop_ms": round(st32["loop_ms"], 3), "iter_count": it32,
+            "published_ms": {"Xeon Platinum 8358": 126, "i9-10920X": 510, "Xeon Gold 6128": 339,
+                             "Xeon E5-2686 v4": 3759, "Iris Xe MAX": 2509, "UHD P630": 8259},
+            "speedup_vs_fastest_published": round(126.0 / (st32["h2d_ms"] + st32["loop_ms"]), 1)}
+
     # ---- CPU baseline (rank 0, N = 1) ------------------------------------
     if world == 1 and rank == 0 and not args.no_cpu:
         from oracle import oracle as orc
