@@ -624,6 +624,37 @@ def test_fuzz_vs_oracle(eigen, orc):
         assert np.max(np.abs(v - ref.eigen_vec)) <= (1e-10 if dt == np.float64 else 5e-4), tag
 
 
+def test_config1_hilbert8192_fp64_vs_oracle(solver, orc):
+    """BASELINE configs[1]: 8192² Hilbert fp64 on one GPU, both forms, vs
+    the oracle's same-semantics solve (17 rounds, README.md:76)."""
+    a = dev.generate("hilbert", 8192, torch.float64, device=DEV)
+    ref = orc.similarity_transform(orc.hilbert(8192), orc.SEM_SYCL, nthreads=16)
+    assert ref.iter_count == 17
+    for mf in (False, True):
+        lam, v, it, st = solver.solve(a, matrix_free=mf)
+        assert it == 17 and st["rounds"] == 18
+        assert abs(lam - ref.eigen_val) <= 1e-12 * ref.eigen_val
+        assert np.max(np.abs(to_np(v) - ref.eigen_vec)) <= 1e-12
+
+
+def test_config5_fp32_32768_tracks_fp64(solver):
+    """BASELINE configs[4]: 32768² fp32 (float4 accesses) over a fixed
+    number of rounds agrees with the fp64 iteration on the same input to
+    fp32 precision (the tolerance study, profiles/r01_fp32_study.json)."""
+    n = 32768
+    a32 = dev.generate("random", n, torch.float32, seed=0, device=DEV)
+    lam32, v32, it32, _ = solver.solve(a32, inplace=True, eps=0.0, max_itr=8)
+    del a32
+    torch.cuda.empty_cache()
+    a64 = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    lam64, v64, it64, _ = solver.solve(a64, inplace=True, eps=0.0, max_itr=8)
+    del a64
+    torch.cuda.empty_cache()
+    assert it32 == it64 == 8
+    assert abs(lam32 - lam64) <= 1e-6 * lam64
+    assert (v32.double() - v64).abs().max().item() <= 1e-5
+
+
 def test_cpp_kernel_tests():
     # tests/cpp/test_kernels.cpp mirrors the reference's tests/test.cpp
     import subprocess
