@@ -53,9 +53,9 @@ for s in $STEPS; do
       # belongs to a single launch shape: configs[1] and the north-star size
       for W in "hilbert 8192" "random 32768"; do
         set -- $W; K=$1; N=$2; D="$OUT/${K}${N}"
-        step "prof_${K}${N}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind $K --n $N --no-cpu --no-north-star
-        step "pmc_fetch_${K}${N}" 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star
-        step "pmc_write_${K}${N}" 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star
+        step "prof_${K}${N}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind $K --n $N --no-cpu --no-north-star --no-headline
+        step "pmc_fetch_${K}${N}" 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
+        step "pmc_write_${K}${N}" 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
         python3 tools/pmc_traffic.py --workload "${K}${N}_f64" --n $N --fetch "$D/pmc_fetch/run_counter_collection.csv" --write "$D/pmc_write/run_counter_collection.csv" --trace "$D/prof/run_kernel_trace.csv" --out "$D/pmc.json" | tee -a "$OUT/session.log"
       done ;;
   esac

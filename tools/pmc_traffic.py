@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--workload", required=True)
     ap.add_argument("--n", type=int, required=True)
     ap.add_argument("--elem", type=int, default=8)
+    ap.add_argument("--dtype", default="double", help="template element type to keep")
     ap.add_argument("--fetch", required=True)
     ap.add_argument("--write", required=True)
     ap.add_argument("--trace")
@@ -60,7 +61,7 @@ def main():
     entries = []
     for key in sorted(fetch):
         kname, full = key
-        if kname not in algo:
+        if kname not in algo or f"<{a.dtype}," not in full:
             continue
         f = fetch[key]
         w = write.get(key, [])
