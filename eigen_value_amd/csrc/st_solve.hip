@@ -178,17 +178,24 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   T* vb[2] = { d_v, d_v2 };
   const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
   const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
-  std::vector<hipEvent_t> ev; // [rowsum_a, rowsum_b, (k1_a, k1_b)*]
+  // timing events [rowsum_a, rowsum_b, (round_a, round_b)*], destroyed on
+  // every exit path
+  struct Events
+  {
+    std::vector<hipEvent_t> e;
+    ~Events()
+    {
+      for (hipEvent_t x : e)
+        if (x)
+          (void)hipEventDestroy(x);
+    }
+  } events;
+  std::vector<hipEvent_t>& ev = events.e;
   auto mk = [&](hipEvent_t* e) -> int {
     ST_CHECK(hipEventCreate(e));
     return 0;
   };
   int rc = 0;
-  auto cleanup = [&]() {
-    for (hipEvent_t e : ev)
-      if (e)
-        (void)hipEventDestroy(e);
-  };
 
   const auto t0 = std::chrono::steady_clock::now();
   ST_CHECK(hipMemsetAsync(c->d_state, 0, sizeof(st_state), s));
@@ -196,16 +203,12 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     return -1;
   if (timed) {
     ev.resize(2, nullptr);
-    if (mk(&ev[0]) || mk(&ev[1])) {
-      cleanup();
+    if (mk(&ev[0]) || mk(&ev[1]))
       return -1;
-    }
     (void)hipEventRecord(ev[0], s);
   }
-  if (launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) { // K0
-    cleanup();
+  if (launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) // K0
     return -1;
-  }
   if (timed)
     (void)hipEventRecord(ev[1], s);
 
@@ -234,10 +237,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
       if (timed)
         (void)hipEventRecord(eb, s);
       cur ^= 1;
-      if (rc) {
-        cleanup();
+      if (rc)
         return -1;
-      }
     }
     enqueued += b;
     const int slot = batch_no & 1;
@@ -292,7 +293,6 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
       stats->fused_launches = transforms;
     }
   }
-  cleanup();
   return (int64_t)loop_ms;
 }
 
