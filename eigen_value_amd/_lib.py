@@ -136,6 +136,15 @@ def _declare(L: ctypes.CDLL) -> None:
         for name in ("generate_hilbert", "generate_random", "generate_identity",
                      "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
+    L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
+    L.st_comm_unique_id.restype = i32
+    L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]
+    L.st_comm_init.restype = i32
+    L.st_comm_destroy.argtypes = [P]
+    L.st_comm_destroy.restype = i32
+    for sfx in ("f32", "f64"):
+        getattr(L, f"st_allgather_{sfx}").argtypes = [P, P, P, u64, P]
+        getattr(L, f"st_allgather_{sfx}").restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32
 

@@ -324,4 +324,70 @@ st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
                                  eigen_val, eigen_vec, iter_cnt, opt, stats);
 }
 
+// ---------------------------------------------------------------------------
+// one-process-per-GPU communicator (the sharded driver's RCCL path): rank 0
+// makes the 128-byte unique id, the caller broadcasts it (torch.distributed
+// over TCP), every rank joins; the all-gather is then issued directly on
+// the launch stream, with no cross-stream hand-off per round.
+// ---------------------------------------------------------------------------
+int
+st_comm_unique_id(char* id_out /* NCCL_UNIQUE_ID_BYTES */)
+{
+  st::clear_error();
+  ST_REQUIRE(id_out, "st_comm_unique_id: null output");
+  ncclUniqueId id;
+  ST_NCCL(ncclGetUniqueId(&id));
+  std::memcpy(id_out, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+int
+st_comm_init(void** comm, int nranks, int rank, const char* id_in, int device)
+{
+  st::clear_error();
+  ST_REQUIRE(comm && id_in, "st_comm_init: null pointer");
+  ST_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "st_comm_init: bad rank");
+  *comm = nullptr;
+  ST_CHECK(hipSetDevice(device));
+  ncclUniqueId id;
+  std::memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t c = nullptr;
+  ST_NCCL(ncclCommInitRank(&c, nranks, id, rank));
+  *comm = c;
+  return 0;
+}
+
+int
+st_comm_destroy(void* comm)
+{
+  st::clear_error();
+  if (comm)
+    ST_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+  return 0;
+}
+
+int
+st_allgather_f32(void* comm, const float* send, float* recv, uint64_t count,
+                 void* stream)
+{
+  st::clear_error();
+  ST_REQUIRE(comm && send && recv, "st_allgather: null pointer");
+  ST_NCCL(ncclAllGather(send, recv, count, ncclFloat,
+                        reinterpret_cast<ncclComm_t>(comm),
+                        reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
+int
+st_allgather_f64(void* comm, const double* send, double* recv, uint64_t count,
+                 void* stream)
+{
+  st::clear_error();
+  ST_REQUIRE(comm && send && recv, "st_allgather: null pointer");
+  ST_NCCL(ncclAllGather(send, recv, count, ncclDouble,
+                        reinterpret_cast<ncclComm_t>(comm),
+                        reinterpret_cast<hipStream_t>(stream)));
+  return 0;
+}
+
 } // extern "C"

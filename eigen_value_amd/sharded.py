@@ -98,6 +98,46 @@ class HipShardOps:
         return self.dev.read_state(state)
 
 
+class RcclComm:
+    """An RCCL communicator owned by libsimilarity_transform.so for the
+    per-round all-gather: the unique id is made by rank 0 and broadcast over
+    the existing torch.distributed group; the collective is then issued
+    straight on the launch stream (no per-round hand-off between torch's
+    compute and communication streams)."""
+
+    def __init__(self, group=None, device_index: Optional[int] = None):
+        import ctypes
+
+        import torch
+        import torch.distributed as dist
+        self.ctypes, self.torch = ctypes, torch
+        self.L = _lib.load()
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        dev = torch.cuda.current_device() if device_index is None else device_index
+        uid = ctypes.create_string_buffer(128)
+        if rank == 0:
+            _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
+        obj = [uid.raw if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
+                                   group=group)
+        self.comm = ctypes.c_void_p()
+        _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, obj[0], dev),
+                   "st_comm_init")
+        self.rank, self.world = rank, world
+
+    def allgather(self, out, inp) -> None:
+        sfx = "f64" if out.dtype == self.torch.float64 else "f32"
+        stream = self.torch.cuda.current_stream(out.device).cuda_stream
+        _lib.check(getattr(self.L, f"st_allgather_{sfx}")(
+            self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), stream), "st_allgather")
+
+    def close(self) -> None:
+        if self.comm is not None and self.comm.value:
+            self.L.st_comm_destroy(self.comm)
+            self.comm = self.ctypes.c_void_p()
+
+
 def _allgather(out, inp, group=None):
     """out[rank*chunk:(rank+1)*chunk] <- inp on every rank (in-place safe)."""
     import torch.distributed as dist
@@ -113,7 +153,8 @@ class ShardedSimilarityTransform:
     """The round loop of similarity_transform.cpp:34-66 over P row blocks."""
 
     def __init__(self, n: int, dtype=None, group=None, ops=None,
-                 semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False):
+                 semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False,
+                 comm: str = "auto"):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -136,6 +177,21 @@ class ShardedSimilarityTransform:
         self.mat = None
         self.k = 0
         self.cur = 0
+        # the per-round exchange: RCCL owned by the library ("native", the
+        # default for an nccl group on the GPU ops), or torch.distributed
+        self.rccl = None
+        if comm not in ("auto", "native", "torch"):
+            raise ValueError(f"comm must be auto, native or torch, not {comm!r}")
+        if world > 1 and comm != "torch" and isinstance(self.ops, HipShardOps) \
+                and dist.get_backend(group) == "nccl":
+            try:
+                self.rccl = RcclComm(group)
+            except Exception as e:          # auto: keep torch's RCCL group
+                if comm == "native":
+                    raise
+                import warnings
+                warnings.warn(f"library RCCL communicator unavailable ({e}); "
+                              "using torch.distributed all_gather_into_tensor")
 
     # local slot of a gathered vector
     def _slot(self, s):
@@ -156,7 +212,11 @@ class ShardedSimilarityTransform:
         """All-gather the padded per-rank slots of s (one RCCL call)."""
         p = self.part
         if p.world > 1:
-            _allgather(s, s[p.rank * p.chunk:(p.rank + 1) * p.chunk], self.group)
+            slot = s[p.rank * p.chunk:(p.rank + 1) * p.chunk]
+            if self.rccl is not None:
+                self.rccl.allgather(s, slot)
+            else:
+                _allgather(s, slot, self.group)
 
     def start(self):
         """v = 1, state = 0, s_0 = rowsum(A_0) gathered (the initial pass)."""

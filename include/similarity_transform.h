@@ -159,6 +159,19 @@ int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
                            unsigned int* iter_cnt, const st_options* opt,
                            st_stats* stats);
 
+/* One-process-per-GPU RCCL communicator for the sharded step API: rank 0
+ * calls st_comm_unique_id (128 bytes), the caller distributes the id, every
+ * rank calls st_comm_init (nranks, its rank, its HIP device).  st_allgather
+ * is ncclAllGather on `stream` (in place when send = recv + rank*count). */
+int st_comm_unique_id(char* id_out);
+int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
+                 int device);
+int st_comm_destroy(void* comm);
+int st_allgather_f32(void* comm, const float* send, float* recv,
+                     uint64_t count, void* stream);
+int st_allgather_f64(void* comm, const double* send, double* recv,
+                     uint64_t count, void* stream);
+
 /* ---------------------------------------------------------------------- */
 /* 4. step-level kernels (asynchronous on `stream`, a hipStream_t or NULL) */
 /* ---------------------------------------------------------------------- */
