@@ -551,6 +551,15 @@ def _rccl_worker(rank, port, outdir):
         out = torch.arange(12, dtype=torch.float64, device="cuda")
         _allgather(out, out[0:12])
         assert torch.equal(out, torch.arange(12, dtype=torch.float64, device="cuda"))
+        # the library-owned communicator (id broadcast over the group)
+        from eigen_value_amd.sharded import RcclComm
+        rc = RcclComm()
+        for dt in (torch.float64, torch.float32):
+            out = torch.arange(12, dtype=dt, device="cuda")
+            rc.allgather(out, out[0:12])
+            torch.cuda.synchronize()
+            assert torch.equal(out, torch.arange(12, dtype=dt, device="cuda"))
+        rc.close()
         sh = ShardedSimilarityTransform(2048, torch.float64)
         sh.load("hilbert")
         lam, v, iters, rounds = sh.solve()
