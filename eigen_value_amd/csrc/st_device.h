@@ -346,7 +346,7 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 }
 
 template <typename T, int ROWS, int W, int U, int ORDER, bool NT,
-          int BLK = kBlock>
+          int BLK = kBlock, bool ALT = false>
 __global__ __launch_bounds__(BLK) void
 k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
         T* __restrict__ v, uint32_t ng_main, uint32_t nrem, uint32_t ncols,
@@ -370,8 +370,16 @@ k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
   T dummy_mx = 0;
   int dummy_ok = 1;
 
-  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const bool first = g == blockIdx.x;
+  // ALT: on odd rounds every workgroup walks its own row groups backwards,
+  // so a round starts on the rows the previous round wrote last (still in
+  // the memory-side cache) while each workgroup keeps the same rows (and
+  // XCD) every round
+  const uint32_t cnt =
+    blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const bool rev = ALT && (k & 1u);
+  for (uint32_t i = 0; i < cnt; i++) {
+    const bool first = i == 0;
+    const uint32_t g = blockIdx.x + (rev ? cnt - 1 - i : i) * gridDim.x;
     if (g < ng_main) {
       if (first)
         round_group<T, ROWS, W, U, ORDER, NT, BLK, true>(
@@ -544,7 +552,8 @@ mfree_group(const T* a0, const T* __restrict__ s_prev,
   __syncthreads();
 }
 
-template <typename T, int ROWS, int W, int U, bool NT, int BLK = kBlock>
+template <typename T, int ROWS, int W, int U, bool NT, int BLK = kBlock,
+          bool ALT = false>
 __global__ __launch_bounds__(BLK) void
 k_mfree(const T* a0, const T* __restrict__ s_prev, T* __restrict__ s_next,
         const T* __restrict__ v_prev, T* __restrict__ v_cur, uint32_t ng_main,
@@ -567,8 +576,12 @@ k_mfree(const T* a0, const T* __restrict__ s_prev, T* __restrict__ s_next,
   int ok = 1;
   T dmx = 0;
   int dok = 1;
-  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const bool first = g == blockIdx.x;
+  const uint32_t cnt = // as k_round
+    blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  const bool rev = ALT && (k & 1u);
+  for (uint32_t i = 0; i < cnt; i++) {
+    const bool first = i == 0;
+    const uint32_t g = blockIdx.x + (rev ? cnt - 1 - i : i) * gridDim.x;
     if (g < ng_main) {
       if (first)
         mfree_group<T, ROWS, W, U, NT, BLK, true>(a0, s_prev, v_prev, s_next,

@@ -38,51 +38,87 @@ check_launch(const char* what)
   return 0;
 }
 
-// Tuned shapes (tools/tune_fused.hip, tools/stream_bench.hip;
-// profiles/r01_tuning.md).  The in-place read+write stream peaks with few
-// streams in flight: 2 rows per group, 2 column chunks of 16 B per lane per
-// row, non-temporal matrix loads/stores, one 256-thread workgroup per CU
-// striding over the row groups (4 rows per group below 1 GiB, where rows
-// are short; 1 row and 2 workgroups per CU below 1024 rows).
-// The read-only matrix-free sweep peaks with 4 rows per group, 2 chunks in
-// flight, 2 workgroups per CU for matrices >= 1 GiB (4 per CU below).
-constexpr int kRows = 2;      // matrices >= 1 GiB
-constexpr int kRowsShort = 4; // below: 4 rows share each group's reduction
+// Tuned shapes (tools/tune_fused.hip, tools/stream_bench.hip,
+// tools/sweep_dir.hip; profiles/README.md).  One 256-thread workgroup
+// streams a group of rows, 2 column chunks of 16 B per lane per row in
+// flight; the grid strides over the row groups.  What pays depends on the
+// size of the (local) matrix relative to the caches — 4 MB L2 per XCD, the
+// 256 MB memory-side cache (MALL) — so the shape is picked per launch:
+//   * matrices that outgrow the MALL (k_round >= 1 GiB, k_mfree >= 512 MiB)
+//     use non-temporal loads/stores; below that, cached accesses let the
+//     MALL serve part of the next round;
+//   * every workgroup keeps the same row groups each round (same XCD, same
+//     L2) and walks them backwards on odd rounds (ALT in st_device.h), so a
+//     round starts on the rows the previous round touched last;
+//   * k_round: 4 rows per group up to 96 KiB rows, 2 above; one workgroup
+//     per CU; 1 row per group and 2 workgroups per CU below 1024 rows.
+//   * k_mfree: 4 rows per group, 2 workgroups per CU (2 rows below 512 MiB).
+constexpr int kRows = 2; // k_fused (K0 row sums and the step API)
 constexpr int kUnroll = 2;
-constexpr bool kNontemporal = true;
 constexpr uint32_t kGridCap = 512;
-constexpr int kMfRows = 4;
 constexpr int kMfUnroll = 2;
-constexpr uint32_t kMfGridCap = 1024;
 
-inline uint32_t
-mfree_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
+struct Shape
 {
-  return (size_t)nrows * ncols * elem >= ((size_t)1 << 30) ? 512u : 1024u;
+  int rows;      // rows per group: 1, 2 or 4
+  bool nt;       // non-temporal matrix loads/stores
+  uint32_t grid; // workgroup cap
+};
+
+inline size_t
+block_bytes(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return (size_t)nrows * ncols * elem;
 }
 
-inline uint32_t
-round_grid_cap(uint32_t nrows, uint32_t ncols, size_t elem)
+inline Shape
+round_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  // one workgroup per CU once the rows are grouped (>= 1024 rows), else two
-  (void)ncols;
-  (void)elem;
-  return nrows >= 2 * kGridCap ? 256u : 512u;
+  const size_t b = block_bytes(nrows, ncols, elem);
+  if (nrows < 2 * kGridCap)
+    return { 1, false, 512u };
+  if (b < ((size_t)128 << 20))
+    return { 2, false, 512u };
+  if (b < ((size_t)1 << 30))
+    return { 4, false, 256u };
+  return { (size_t)ncols * elem <= ((size_t)96 << 10) ? 4 : 2, true, 256u };
+}
+
+inline Shape
+mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  const size_t b = block_bytes(nrows, ncols, elem);
+  if (nrows < 2 * kGridCap)
+    return { 1, false, 1024u };
+  if (b < ((size_t)512 << 20))
+    return { 2, false, 512u };
+  return { 4, true, 512u };
+}
+
+inline bool
+fused_nt(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  // k_fused is the read-mostly K0 row-sum pass: the k_mfree threshold
+  return block_bytes(nrows, ncols, elem) >= ((size_t)512 << 20);
 }
 
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER>
 void
 launch_cfg(T* a, const T* s_cur, T* s_next, uint32_t row_begin,
-           uint32_t nblocks, uint32_t ncols, uint32_t row0,
+           uint32_t nblocks, uint32_t ncols, uint32_t row0, bool nt,
            const st_state* st, hipStream_t stream)
 {
   if (nblocks == 0)
     return;
   const uint32_t grid = nblocks < kGridCap ? nblocks : kGridCap;
-  hipLaunchKernelGGL(
-    (dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, kNontemporal>),
-    dim3(grid), dim3(kBlock), 0, stream, a, a, s_cur, s_next, row_begin,
-    nblocks, ncols, row0, st);
+  if (nt)
+    hipLaunchKernelGGL((dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, true>),
+                       dim3(grid), dim3(kBlock), 0, stream, a, a, s_cur, s_next,
+                       row_begin, nblocks, ncols, row0, st);
+  else
+    hipLaunchKernelGGL((dev::k_fused<T, ROWS, W, U, SCALE, SUM, ORDER, false>),
+                       dim3(grid), dim3(kBlock), 0, stream, a, a, s_cur, s_next,
+                       row_begin, nblocks, ncols, row0, st);
 }
 
 template <typename T, int W, bool SCALE, bool SUM, int ORDER>
@@ -90,17 +126,26 @@ void
 launch_rows(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
             uint32_t row0, const st_state* st, hipStream_t stream)
 {
+  const bool nt = fused_nt(nrows, ncols, sizeof(T));
   // small matrices: one row per workgroup keeps >= 256 workgroups busy
   if (nrows < 2 * kGridCap) {
     launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(a, s_cur, s_next, 0, nrows,
-                                                    ncols, row0, st, stream);
+                                                    ncols, row0, nt, st, stream);
     return;
   }
-  const uint32_t full = nrows / kRows;
-  launch_cfg<T, kRows, W, kUnroll, SCALE, SUM, ORDER>(
-    a, s_cur, s_next, 0, full, ncols, row0, st, stream);
+  // the pure row-sum pass streams like k_mfree: 4 rows per group once the
+  // matrix outgrows the MALL
+  constexpr int R4 = SCALE ? kRows : 4;
+  const int rows = nt ? R4 : kRows;
+  const uint32_t full = nrows / rows;
+  if (rows == 4)
+    launch_cfg<T, R4, W, kUnroll, SCALE, SUM, ORDER>(
+      a, s_cur, s_next, 0, full, ncols, row0, nt, st, stream);
+  else
+    launch_cfg<T, kRows, W, kUnroll, SCALE, SUM, ORDER>(
+      a, s_cur, s_next, 0, full, ncols, row0, nt, st, stream);
   launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(
-    a, s_cur, s_next, full * kRows, nrows - full * kRows, ncols, row0, st,
+    a, s_cur, s_next, full * rows, nrows - full * rows, ncols, row0, nt, st,
     stream);
 }
 
@@ -120,21 +165,20 @@ launch_vec(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
                                          st, stream);
 }
 
-template <typename T, int ROWS, int W, int ORDER>
+template <typename T, int ROWS, int W, int ORDER, bool NT>
 void
 launch_round_cfg(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                  uint32_t ncols, uint32_t row0, T eps, uint32_t k,
                  uint32_t max_itr, uint32_t semantics, st_state* st,
-                 hipStream_t stream)
+                 uint32_t cap, hipStream_t stream)
 {
   const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
   const uint32_t ng = ng_main + nrem;
-  const uint32_t cap = round_grid_cap(nrows, ncols, sizeof(T));
   const uint32_t grid = ng < cap ? ng : cap;
-  hipLaunchKernelGGL((dev::k_round<T, ROWS, W, kUnroll, ORDER, kNontemporal>),
-                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, s_next, v,
-                     ng_main, nrem, ncols, row0, eps, k, max_itr, semantics,
-                     st);
+  hipLaunchKernelGGL(
+    (dev::k_round<T, ROWS, W, kUnroll, ORDER, NT, kBlock, true>), dim3(grid),
+    dim3(kBlock), 0, stream, a, s_cur, s_next, v, ng_main, nrem, ncols, row0,
+    eps, k, max_itr, semantics, st);
 }
 
 template <typename T, int W, int ORDER>
@@ -144,35 +188,55 @@ launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                   uint32_t max_itr, uint32_t semantics, st_state* st,
                   hipStream_t stream)
 {
-  const size_t bytes = (size_t)nrows * ncols * sizeof(T);
-  if (nrows < 2 * kGridCap) // small: one row per group keeps the CUs busy
-    launch_round_cfg<T, 1, W, ORDER>(a, s_cur, s_next, v, nrows, ncols, row0,
-                                     eps, k, max_itr, semantics, st, stream);
-  else if (bytes < ((size_t)1 << 30)) // short rows: amortise the per-group
-    launch_round_cfg<T, kRowsShort, W, ORDER>(a, s_cur, s_next, v, nrows,
-                                              ncols, row0, eps, k, max_itr,
-                                              semantics, st, stream);
+  const Shape sh = round_shape(nrows, ncols, sizeof(T));
+#define ST_ROUND_CFG(R, N)                                                     \
+  launch_round_cfg<T, R, W, ORDER, N>(a, s_cur, s_next, v, nrows, ncols, row0, \
+                                      eps, k, max_itr, semantics, st, sh.grid, \
+                                      stream)
+  if (sh.rows == 1)
+    ST_ROUND_CFG(1, false);
+  else if (sh.rows == 2)
+    sh.nt ? ST_ROUND_CFG(2, true) : ST_ROUND_CFG(2, false);
   else
-    launch_round_cfg<T, kRows, W, ORDER>(a, s_cur, s_next, v, nrows, ncols,
-                                         row0, eps, k, max_itr, semantics, st,
-                                         stream);
+    sh.nt ? ST_ROUND_CFG(4, true) : ST_ROUND_CFG(4, false);
+#undef ST_ROUND_CFG
 }
 
-template <typename T, int ROWS, int W>
+template <typename T, int ROWS, int W, bool NT>
 void
 launch_mfree_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
                  T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,
                  T eps, uint32_t k, uint32_t max_itr, uint32_t semantics,
-                 st_state* st, hipStream_t stream)
+                 st_state* st, uint32_t cap, hipStream_t stream)
 {
   const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
   const uint32_t ng = ng_main + nrem;
-  const uint32_t cap = mfree_grid_cap(nrows, ncols, sizeof(T));
   const uint32_t grid = ng < cap ? ng : cap;
-  hipLaunchKernelGGL((dev::k_mfree<T, ROWS, W, kMfUnroll, kNontemporal>),
-                     dim3(grid), dim3(kBlock), 0, stream, a0, s_prev, s_next,
-                     v_prev, v_cur, ng_main, nrem, ncols, row0, eps, k,
-                     max_itr, semantics, st);
+  hipLaunchKernelGGL(
+    (dev::k_mfree<T, ROWS, W, kMfUnroll, NT, kBlock, true>), dim3(grid),
+    dim3(kBlock), 0, stream, a0, s_prev, s_next, v_prev, v_cur, ng_main, nrem,
+    ncols, row0, eps, k, max_itr, semantics, st);
+}
+
+template <typename T, int W>
+void
+launch_mfree_rows(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
+                  T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,
+                  T eps, uint32_t k, uint32_t max_itr, uint32_t semantics,
+                  st_state* st, hipStream_t stream)
+{
+  const Shape sh = mfree_shape(nrows, ncols, sizeof(T));
+#define ST_MFREE_CFG(R, N)                                                     \
+  launch_mfree_cfg<T, R, W, N>(a0, s_prev, s_next, v_prev, v_cur, nrows,       \
+                               ncols, row0, eps, k, max_itr, semantics, st,    \
+                               sh.grid, stream)
+  if (sh.rows == 1)
+    ST_MFREE_CFG(1, false);
+  else if (sh.rows == 2)
+    sh.nt ? ST_MFREE_CFG(2, true) : ST_MFREE_CFG(2, false);
+  else
+    sh.nt ? ST_MFREE_CFG(4, true) : ST_MFREE_CFG(4, false);
+#undef ST_MFREE_CFG
 }
 
 } // namespace
@@ -193,26 +257,12 @@ launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
   constexpr int W = 16 / sizeof(T);
   const bool vec_ok = (ncols % W) == 0 && aligned16(a0) && aligned16(s_prev) &&
                       aligned16(v_prev);
-  const bool small = nrows < 2 * kMfGridCap; // keep >= 2 rows per workgroup
-  if (vec_ok) {
-    if (small)
-      launch_mfree_cfg<T, 1, W>(a0, s_prev, s_next, v_prev, v_cur, nrows,
-                                ncols, row0, eps, k, max_itr, semantics, st,
-                                stream);
-    else
-      launch_mfree_cfg<T, kMfRows, W>(a0, s_prev, s_next, v_prev, v_cur, nrows,
-                                      ncols, row0, eps, k, max_itr, semantics,
-                                      st, stream);
-  } else {
-    if (small)
-      launch_mfree_cfg<T, 1, 1>(a0, s_prev, s_next, v_prev, v_cur, nrows,
-                                ncols, row0, eps, k, max_itr, semantics, st,
-                                stream);
-    else
-      launch_mfree_cfg<T, kMfRows, 1>(a0, s_prev, s_next, v_prev, v_cur, nrows,
-                                      ncols, row0, eps, k, max_itr, semantics,
-                                      st, stream);
-  }
+  if (vec_ok)
+    launch_mfree_rows<T, W>(a0, s_prev, s_next, v_prev, v_cur, nrows, ncols,
+                            row0, eps, k, max_itr, semantics, st, stream);
+  else
+    launch_mfree_rows<T, 1>(a0, s_prev, s_next, v_prev, v_cur, nrows, ncols,
+                            row0, eps, k, max_itr, semantics, st, stream);
   return check_launch("mfree");
 }
 

@@ -1,0 +1,209 @@
+// sweep_dir.hip — does alternating the sweep direction between rounds pay?
+//
+// A round rewrites the whole matrix; the rows written last may still sit in
+// the MI355X memory-side cache (MALL, 256 MB) when the next round starts.
+// Forward-every-round sweeps start on the rows written FIRST (long evicted);
+// alternating forward/backward starts on the rows written LAST.  This tool
+// times sequences of consecutive rounds (k = 0, 1, 2, ...) of k_round and
+// k_mfree with ALT off/on, NT on/off, plus a plain in-place stream pass for
+// reference, at the sizes given on the command line.
+//
+// Build: make -C tools sweep_dir   Run: ./tools/sweep_dir 8192 16384 32768
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "st_device.h"
+
+using namespace st::dev;
+
+#define HIPCHECK(x)                                                            \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,           \
+                   hipGetErrorString(e));                                      \
+      std::exit(2);                                                            \
+    }                                                                          \
+  } while (0)
+
+template <typename T, bool NT>
+__global__ __launch_bounds__(256) void
+k_stream_rw(T* __restrict__ a, size_t n, T f, int rev)
+{
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * 256) {
+    const size_t j = rev ? n - 1 - i : i;
+    T x;
+    if constexpr (NT)
+      x = __builtin_nontemporal_load(a + j);
+    else
+      x = a[j];
+    x *= f;
+    if constexpr (NT)
+      __builtin_nontemporal_store(x, a + j);
+    else
+      a[j] = x;
+  }
+}
+
+constexpr int kSeq = 16; // rounds per timed sequence
+constexpr int kReps = 7; // sequences; median reported
+
+template <typename F>
+static float
+time_seq(F launch)
+{
+  hipEvent_t a, b;
+  HIPCHECK(hipEventCreate(&a));
+  HIPCHECK(hipEventCreate(&b));
+  for (int k = 0; k < kSeq; k++)
+    launch(k);
+  HIPCHECK(hipDeviceSynchronize());
+  std::vector<float> t;
+  for (int r = 0; r < kReps; r++) {
+    HIPCHECK(hipEventRecord(a));
+    for (int k = 0; k < kSeq; k++)
+      launch(k);
+    HIPCHECK(hipEventRecord(b));
+    HIPCHECK(hipEventSynchronize(b));
+    float ms;
+    HIPCHECK(hipEventElapsedTime(&ms, a, b));
+    t.push_back(ms / kSeq);
+  }
+  HIPCHECK(hipEventDestroy(a));
+  HIPCHECK(hipEventDestroy(b));
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+template <typename T>
+struct Bufs
+{
+  unsigned n;
+  T *a, *s, *sn, *v, *v2;
+  st_state* st;
+};
+
+template <typename T, int ROWS, bool NT, bool ALT>
+static void
+round_seq(const Bufs<T>& b, unsigned cap)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ng = b.n / ROWS;
+  const unsigned grid = cap < ng ? cap : ng;
+  float ms = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round<T, ROWS, W, 2, 0, NT, 256, ALT>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng, 0u, b.n, 0u,
+                       (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+  });
+  const double bytes = 2.0 * b.n * (double)b.n * sizeof(T);
+  std::printf("  k_round rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s\n",
+              ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9);
+}
+
+template <typename T, int ROWS, bool NT, bool ALT>
+static void
+mfree_seq(const Bufs<T>& b, unsigned cap)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ng = b.n / ROWS;
+  const unsigned grid = cap < ng ? cap : ng;
+  float ms = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_mfree<T, ROWS, W, 2, NT, 256, ALT>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, b.sn, b.v, b.v2, ng, 0u,
+                       b.n, 0u, (T)0, (uint32_t)(k + 1), 1u << 30, 0u, b.st);
+  });
+  const double bytes = 1.0 * b.n * (double)b.n * sizeof(T);
+  std::printf("  k_mfree rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s\n",
+              ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9);
+}
+
+template <typename T, bool NT>
+static void
+stream_seq(const Bufs<T>& b, bool alt)
+{
+  const size_t nn = (size_t)b.n * b.n;
+  float ms = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_stream_rw<T, NT>), dim3(2048), dim3(256), 0, 0, b.a,
+                       nn, (T)1, alt ? (k & 1) : 0);
+  });
+  std::printf("  stream_rw nt=%d alt=%d            %8.4f ms  %7.1f GB/s\n",
+              (int)NT, (int)alt, ms, 2.0 * nn * sizeof(T) / (ms * 1e-3) / 1e9);
+}
+
+template <typename T>
+static void
+run(unsigned n)
+{
+  Bufs<T> b;
+  b.n = n;
+  const size_t nn = (size_t)n * n;
+  HIPCHECK(hipMalloc(&b.a, nn * sizeof(T)));
+  HIPCHECK(hipMalloc(&b.s, n * sizeof(T)));
+  HIPCHECK(hipMalloc(&b.sn, n * sizeof(T)));
+  HIPCHECK(hipMalloc(&b.v, n * sizeof(T)));
+  HIPCHECK(hipMalloc(&b.v2, n * sizeof(T)));
+  HIPCHECK(hipMalloc(&b.st, sizeof(st_state)));
+  HIPCHECK(hipMemset(b.st, 0, sizeof(st_state)));
+  hipLaunchKernelGGL((k_generate<T, kRandom>), dim3(65536), dim3(256), 0, 0,
+                     b.a, n, n, 0u, 0ull);
+  hipLaunchKernelGGL(k_fill<T>, dim3(256), dim3(256), 0, 0, b.s, (uint64_t)n,
+                     (T)1);
+  hipLaunchKernelGGL(k_fill<T>, dim3(256), dim3(256), 0, 0, b.v, (uint64_t)n,
+                     (T)1);
+  HIPCHECK(hipDeviceSynchronize());
+  std::printf("n=%u %s  matrix %.3f GiB\n", n, sizeof(T) == 8 ? "f64" : "f32",
+              nn * sizeof(T) / (double)(1u << 30));
+  stream_seq<T, true>(b, false);
+  stream_seq<T, true>(b, true);
+  stream_seq<T, false>(b, false);
+  stream_seq<T, false>(b, true);
+  for (unsigned cap : { 256u, 512u, 1024u }) {
+    round_seq<T, 2, true, false>(b, cap);
+    round_seq<T, 2, true, true>(b, cap);
+    round_seq<T, 2, false, false>(b, cap);
+    round_seq<T, 2, false, true>(b, cap);
+    round_seq<T, 4, true, false>(b, cap);
+    round_seq<T, 4, true, true>(b, cap);
+    round_seq<T, 4, false, false>(b, cap);
+    round_seq<T, 4, false, true>(b, cap);
+  }
+  for (unsigned cap : { 512u, 1024u, 2048u }) {
+    mfree_seq<T, 2, true, false>(b, cap);
+    mfree_seq<T, 2, false, false>(b, cap);
+    mfree_seq<T, 2, false, true>(b, cap);
+    mfree_seq<T, 4, true, false>(b, cap);
+    mfree_seq<T, 4, true, true>(b, cap);
+    mfree_seq<T, 4, false, false>(b, cap);
+    mfree_seq<T, 4, false, true>(b, cap);
+  }
+  HIPCHECK(hipFree(b.a));
+  HIPCHECK(hipFree(b.s));
+  HIPCHECK(hipFree(b.sn));
+  HIPCHECK(hipFree(b.v));
+  HIPCHECK(hipFree(b.v2));
+  HIPCHECK(hipFree(b.st));
+}
+
+int
+main(int argc, char** argv)
+{
+  std::vector<unsigned> ns;
+  for (int i = 1; i < argc; i++)
+    ns.push_back((unsigned)std::atoi(argv[i]));
+  if (ns.empty())
+    ns = { 8192u, 16384u, 32768u };
+  for (unsigned n : ns) {
+    if (n == 0 || n % 1024) {
+      std::fprintf(stderr, "n must be a positive multiple of 1024\n");
+      return 1;
+    }
+    run<double>(n);
+    run<float>(n);
+  }
+  return 0;
+}
