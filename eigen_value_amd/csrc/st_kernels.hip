@@ -50,8 +50,8 @@ check_launch(const char* what)
 //   * every workgroup keeps the same row groups each round (same XCD, same
 //     L2) and walks them backwards on odd rounds (ALT in st_device.h), so a
 //     round starts on the rows the previous round touched last;
-//   * k_round: 4 rows per group up to 96 KiB rows, 2 above; one workgroup
-//     per CU; 1 row per group and 2 workgroups per CU below 1024 rows.
+//   * k_round: 4 rows per group while rows are short (<= 96 KiB streamed,
+//     <= 12288 columns cached), 2 above; one workgroup per CU; 1 row per group and 2 workgroups per CU below 1024 rows.
 //   * k_mfree: 4 rows per group, 2 workgroups per CU (2 rows below 512 MiB).
 constexpr int kRows = 2; // k_fused (K0 row sums and the step API)
 constexpr int kUnroll = 2;
@@ -77,10 +77,12 @@ round_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   const size_t b = block_bytes(nrows, ncols, elem);
   if (nrows < 2 * kGridCap)
     return { 1, false, 512u };
+  if (b <= ((size_t)32 << 20)) // L2-sized: one group per workgroup
+    return { 2, false, 1024u };
   if (b < ((size_t)128 << 20))
     return { 2, false, 512u };
-  if (b < ((size_t)1 << 30))
-    return { 4, false, 256u };
+  if (b < ((size_t)1 << 30)) // 4 rows per group only while rows are short
+    return { ncols <= 12288u ? 4 : 2, false, 256u };
   return { (size_t)ncols * elem <= ((size_t)96 << 10) ? 4 : 2, true, 256u };
 }
 
@@ -90,6 +92,8 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   const size_t b = block_bytes(nrows, ncols, elem);
   if (nrows < 2 * kGridCap)
     return { 1, false, 1024u };
+  if (b <= ((size_t)64 << 20))
+    return { 4, false, 512u };
   if (b < ((size_t)512 << 20))
     return { 2, false, 512u };
   return { 4, true, 512u };

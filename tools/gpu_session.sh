@@ -40,7 +40,7 @@ for s in $STEPS; do
       step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu
       step pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- python3 bench.py --steps 5 --warmup 1 --no-cpu ;;
     tune)  step tune 600 ./tools/tune_fused ;;
-    sweep) step sweep_dir 600 ./tools/sweep_dir 2048 4096 6144 8192 12288 16384 24576 32768 ;;
+    sweep) step sweep_dir 600 ./tools/sweep_dir ${SWEEP_ARGS:-2048 4096 6144 8192 12288 16384 24576 32768} ;;
     hilbert)
       make -s -C tools bench_hilbert
       step bench_hilbert_f32 300 ./tools/bench_hilbert f32

@@ -9,6 +9,7 @@
 // reference, at the sizes given on the command line.
 //
 // Build: make -C tools sweep_dir   Run: ./tools/sweep_dir 8192 16384 32768
+//        (or RxN: a sharded rank's R-row block of an N-column matrix)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -83,7 +84,8 @@ time_seq(F launch)
 template <typename T>
 struct Bufs
 {
-  unsigned n;
+  unsigned n;  // columns
+  unsigned nr; // rows (a sharded rank's block: nr < n)
   T *a, *s, *sn, *v, *v2;
   st_state* st;
 };
@@ -93,14 +95,14 @@ static void
 round_seq(const Bufs<T>& b, unsigned cap)
 {
   constexpr int W = 16 / sizeof(T);
-  const unsigned ng = b.n / ROWS;
+  const unsigned ng = b.nr / ROWS;
   const unsigned grid = cap < ng ? cap : ng;
   float ms = time_seq([&](int k) {
     hipLaunchKernelGGL((k_round<T, ROWS, W, 2, 0, NT, 256, ALT>), dim3(grid),
                        dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng, 0u, b.n, 0u,
                        (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
   });
-  const double bytes = 2.0 * b.n * (double)b.n * sizeof(T);
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
   std::printf("  k_round rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s\n",
               ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9);
 }
@@ -110,14 +112,14 @@ static void
 mfree_seq(const Bufs<T>& b, unsigned cap)
 {
   constexpr int W = 16 / sizeof(T);
-  const unsigned ng = b.n / ROWS;
+  const unsigned ng = b.nr / ROWS;
   const unsigned grid = cap < ng ? cap : ng;
   float ms = time_seq([&](int k) {
     hipLaunchKernelGGL((k_mfree<T, ROWS, W, 2, NT, 256, ALT>), dim3(grid),
                        dim3(256), 0, 0, b.a, b.s, b.sn, b.v, b.v2, ng, 0u,
                        b.n, 0u, (T)0, (uint32_t)(k + 1), 1u << 30, 0u, b.st);
   });
-  const double bytes = 1.0 * b.n * (double)b.n * sizeof(T);
+  const double bytes = 1.0 * b.nr * (double)b.n * sizeof(T);
   std::printf("  k_mfree rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s\n",
               ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9);
 }
@@ -126,7 +128,7 @@ template <typename T, bool NT>
 static void
 stream_seq(const Bufs<T>& b, bool alt)
 {
-  const size_t nn = (size_t)b.n * b.n;
+  const size_t nn = (size_t)b.nr * b.n;
   float ms = time_seq([&](int k) {
     hipLaunchKernelGGL((k_stream_rw<T, NT>), dim3(2048), dim3(256), 0, 0, b.a,
                        nn, (T)1, alt ? (k & 1) : 0);
@@ -137,11 +139,12 @@ stream_seq(const Bufs<T>& b, bool alt)
 
 template <typename T>
 static void
-run(unsigned n)
+run(unsigned nr, unsigned n)
 {
   Bufs<T> b;
   b.n = n;
-  const size_t nn = (size_t)n * n;
+  b.nr = nr;
+  const size_t nn = (size_t)nr * n;
   HIPCHECK(hipMalloc(&b.a, nn * sizeof(T)));
   HIPCHECK(hipMalloc(&b.s, n * sizeof(T)));
   HIPCHECK(hipMalloc(&b.sn, n * sizeof(T)));
@@ -150,14 +153,19 @@ run(unsigned n)
   HIPCHECK(hipMalloc(&b.st, sizeof(st_state)));
   HIPCHECK(hipMemset(b.st, 0, sizeof(st_state)));
   hipLaunchKernelGGL((k_generate<T, kRandom>), dim3(65536), dim3(256), 0, 0,
-                     b.a, n, n, 0u, 0ull);
+                     b.a, nr, n, 0u, 0ull);
   hipLaunchKernelGGL(k_fill<T>, dim3(256), dim3(256), 0, 0, b.s, (uint64_t)n,
                      (T)1);
   hipLaunchKernelGGL(k_fill<T>, dim3(256), dim3(256), 0, 0, b.v, (uint64_t)n,
                      (T)1);
   HIPCHECK(hipDeviceSynchronize());
-  std::printf("n=%u %s  matrix %.3f GiB\n", n, sizeof(T) == 8 ? "f64" : "f32",
-              nn * sizeof(T) / (double)(1u << 30));
+  if (nr == n)
+    std::printf("n=%u %s  matrix %.3f GiB\n", n, sizeof(T) == 8 ? "f64" : "f32",
+                nn * sizeof(T) / (double)(1u << 30));
+  else
+    std::printf("n=%ux%u %s  block %.3f GiB\n", nr, n,
+                sizeof(T) == 8 ? "f64" : "f32",
+                nn * sizeof(T) / (double)(1u << 30));
   stream_seq<T, true>(b, false);
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
@@ -192,18 +200,24 @@ run(unsigned n)
 int
 main(int argc, char** argv)
 {
-  std::vector<unsigned> ns;
-  for (int i = 1; i < argc; i++)
-    ns.push_back((unsigned)std::atoi(argv[i]));
-  if (ns.empty())
-    ns = { 8192u, 16384u, 32768u };
-  for (unsigned n : ns) {
-    if (n == 0 || n % 1024) {
-      std::fprintf(stderr, "n must be a positive multiple of 1024\n");
+  // arguments: N (square) or RxN (a rank's row block of an N-column matrix)
+  std::vector<std::pair<unsigned, unsigned>> shapes;
+  for (int i = 1; i < argc; i++) {
+    unsigned r = 0, c = 0;
+    if (std::sscanf(argv[i], "%ux%u", &r, &c) != 2)
+      r = c = (unsigned)std::atoi(argv[i]);
+    shapes.push_back({ r, c });
+  }
+  if (shapes.empty())
+    shapes = { { 8192u, 8192u }, { 16384u, 16384u }, { 32768u, 32768u } };
+  for (auto [r, n] : shapes) {
+    if (r == 0 || r % 64 || n % 64 || r > n) {
+      std::fprintf(stderr, "rows must be a positive multiple of 64 <= cols, "
+                           "cols a multiple of 64\n");
       return 1;
     }
-    run<double>(n);
-    run<float>(n);
+    run<double>(r, n);
+    run<float>(r, n);
   }
   return 0;
 }
