@@ -243,7 +243,14 @@ k_fused(const T* a_in, T* a_out, const T* __restrict__ s_cur,
 // returns at once: state->end = k+1 is set by the stop round, and launch j
 // exits if end != 0 && end <= j (a launch never gates on its own round).
 // ---------------------------------------------------------------------------
-template <typename T, int R, int W, int U, int ORDER, bool NT, int BLK,
+// cache policy of k_round's matrix accesses (bit 0: non-temporal loads,
+// bit 1: non-temporal stores)
+constexpr int kCached = 0;
+constexpr int kNtLoads = 1;
+constexpr int kNtStores = 2;
+constexpr int kNtBoth = 3;
+
+template <typename T, int R, int W, int U, int ORDER, int NT, int BLK,
           bool STATS>
 __device__ __forceinline__ void
 round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
@@ -270,7 +277,7 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     for (int u = 0; u < UU; u++)
 #pragma unroll
       for (int j = 0; j < R; j++)
-        x[u][j] = ld<V, NT>(rows[j] + c + u * BLK);
+        x[u][j] = ld<V, (NT & kNtLoads) != 0>(rows[j] + c + u * BLK);
 #pragma unroll
     for (int u = 0; u < UU; u++)
       sc[u] = sv[c + u * BLK];
@@ -312,7 +319,7 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     for (int u = 0; u < UU; u++)
 #pragma unroll
       for (int j = 0; j < R; j++)
-        st<V, NT>(rows[j] + c + u * BLK, x[u][j]);
+        st<V, (NT & kNtStores) != 0>(rows[j] + c + u * BLK, x[u][j]);
 #pragma unroll
     for (int u = 0; u < UU; u++)
 #pragma unroll
@@ -345,7 +352,7 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
   __syncthreads();
 }
 
-template <typename T, int ROWS, int W, int U, int ORDER, bool NT,
+template <typename T, int ROWS, int W, int U, int ORDER, int NT,
           int BLK = kBlock, bool ALT = false>
 __global__ __launch_bounds__(BLK) void
 k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,

@@ -169,7 +169,7 @@ launch_vec(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
                                          st, stream);
 }
 
-template <typename T, int ROWS, int W, int ORDER, bool NT>
+template <typename T, int ROWS, int W, int ORDER, int NT>
 void
 launch_round_cfg(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                  uint32_t ncols, uint32_t row0, T eps, uint32_t k,
@@ -197,12 +197,14 @@ launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
   launch_round_cfg<T, R, W, ORDER, N>(a, s_cur, s_next, v, nrows, ncols, row0, \
                                       eps, k, max_itr, semantics, st, sh.grid, \
                                       stream)
+  using dev::kCached;
+  using dev::kNtBoth;
   if (sh.rows == 1)
-    ST_ROUND_CFG(1, false);
+    ST_ROUND_CFG(1, kCached);
   else if (sh.rows == 2)
-    sh.nt ? ST_ROUND_CFG(2, true) : ST_ROUND_CFG(2, false);
+    sh.nt ? ST_ROUND_CFG(2, kNtBoth) : ST_ROUND_CFG(2, kCached);
   else
-    sh.nt ? ST_ROUND_CFG(4, true) : ST_ROUND_CFG(4, false);
+    sh.nt ? ST_ROUND_CFG(4, kNtBoth) : ST_ROUND_CFG(4, kCached);
 #undef ST_ROUND_CFG
 }
 

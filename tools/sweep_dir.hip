@@ -5,7 +5,7 @@
 // Forward-every-round sweeps start on the rows written FIRST (long evicted);
 // alternating forward/backward starts on the rows written LAST.  This tool
 // times sequences of consecutive rounds (k = 0, 1, 2, ...) of k_round and
-// k_mfree with ALT off/on, NT on/off, plus a plain in-place stream pass for
+// k_mfree with ALT off/on, cache policies, plus a plain in-place stream pass for
 // reference, at the sizes given on the command line.
 //
 // Build: make -C tools sweep_dir   Run: ./tools/sweep_dir 8192 16384 32768
@@ -90,7 +90,7 @@ struct Bufs
   st_state* st;
 };
 
-template <typename T, int ROWS, bool NT, bool ALT>
+template <typename T, int ROWS, int NT, bool ALT>
 static void
 round_seq(const Bufs<T>& b, unsigned cap)
 {
@@ -170,15 +170,19 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
-  for (unsigned cap : { 256u, 512u, 1024u }) {
-    round_seq<T, 2, true, false>(b, cap);
-    round_seq<T, 2, true, true>(b, cap);
-    round_seq<T, 2, false, false>(b, cap);
-    round_seq<T, 2, false, true>(b, cap);
-    round_seq<T, 4, true, false>(b, cap);
-    round_seq<T, 4, true, true>(b, cap);
-    round_seq<T, 4, false, false>(b, cap);
-    round_seq<T, 4, false, true>(b, cap);
+  // k_round cache policy: nt = 0 cached, 1 non-temporal loads, 2
+  // non-temporal stores, 3 both
+  for (unsigned cap : { 256u, 512u }) {
+    round_seq<T, 2, kNtBoth, false>(b, cap);
+    round_seq<T, 2, kCached, true>(b, cap);
+    round_seq<T, 2, kNtLoads, true>(b, cap);
+    round_seq<T, 2, kNtStores, true>(b, cap);
+    round_seq<T, 2, kNtBoth, true>(b, cap);
+    round_seq<T, 4, kNtBoth, false>(b, cap);
+    round_seq<T, 4, kCached, true>(b, cap);
+    round_seq<T, 4, kNtLoads, true>(b, cap);
+    round_seq<T, 4, kNtStores, true>(b, cap);
+    round_seq<T, 4, kNtBoth, true>(b, cap);
   }
   for (unsigned cap : { 512u, 1024u, 2048u }) {
     mfree_seq<T, 2, true, false>(b, cap);

@@ -142,7 +142,7 @@ round_variant(Timer& tm, int reps, unsigned grid_cap)
   const unsigned ng = g_n / ROWS;
   const unsigned grid = grid_cap && grid_cap < ng ? grid_cap : ng;
   auto f = [&] {
-    hipLaunchKernelGGL((k_round<double, ROWS, 2, U, 0, NT, BLK>), dim3(grid),
+    hipLaunchKernelGGL((k_round<double, ROWS, 2, U, 0, NT ? kNtBoth : kCached, BLK>), dim3(grid),
                        dim3(BLK), 0, 0, g_a, g_s, g_sn, g_v, ng, 0u, g_n, 0u,
                        0.0, 0u, 1u << 30, 0u, g_st);
   };
