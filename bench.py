@@ -78,6 +78,19 @@ def scaled_n(n1: int, world: int) -> int:
     return int(round(n1 * math.sqrt(world) / q)) * q
 
 
+def true_lambda(n, dtype, seed):
+    """Committed CPU Perron root (tests/golden/large_pins.json) or None."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden",
+                        "large_pins.json")
+    try:
+        for c in json.load(open(path))["cases"]:
+            if (c["n"], c["dtype"], c["seed"]) == (n, dtype, seed):
+                return c["lambda"]
+    except (OSError, ValueError, KeyError):
+        pass
+    return None
+
+
 def load_traffic(workload: str, kernel: str = "k_round"):
     """Per-launch HBM bytes of a hot kernel from the committed rocprofv3 PMC
     passes of this workload (profiles/*_pmc.json, tools/pmc_traffic.py;
@@ -269,6 +282,9 @@ def main():
                              "frac": round(ach / HBM_PEAK_GBS, 4), "target_frac": 0.70,
                              "traffic": None if tr is None else tr[0],
                              "solve_iter_count": it_ns, "eigen_val": lam_ns}
+        pin = true_lambda(32768, "f64", 0)
+        if pin is not None:  # CPU Perron root of the same matrix (tests/golden)
+            out["north_star"]["eigen_val_rel_err_vs_true"] = abs(lam_ns - pin) / pin
         del ns
         torch.cuda.empty_cache()
         # the matrix-free form on the same 32768^2 input (N^2*b per round)

@@ -44,3 +44,14 @@ def golden_input(case, orc):
     if case["kind"] == "hilbert":
         return orc.hilbert(case["n"], np.float64)
     return orc.random_matrix(case["n"], case["seed"], np.float64)
+
+
+def large_pin(n, dtype, seed=0):
+    """True Perron root of a full-size seeded random matrix
+    (tests/golden/large_pins.json, make_large_pins.py)."""
+    import json
+    doc = json.load(open(os.path.join(REPO, "tests", "golden", "large_pins.json")))
+    for c in doc["cases"]:
+        if (c["n"], c["dtype"], c["seed"]) == (n, dtype, seed):
+            return c
+    raise KeyError((n, dtype, seed))

@@ -25,7 +25,7 @@ if not torch.cuda.is_available():
 import eigen_value_amd as ev  # noqa: E402
 from eigen_value_amd import _lib  # noqa: E402
 from eigen_value_amd import device as dev  # noqa: E402
-from conftest import golden_input  # noqa: E402
+from conftest import golden_input, large_pin  # noqa: E402
 
 DEV = "cuda:0"
 TD = {np.float64: torch.float64, np.float32: torch.float32}
@@ -388,6 +388,10 @@ def test_full_size_properties(solver):
     lo, hi = q.min().item(), q.max().item()
     assert v.min().item() > 0 and lo <= hi
     assert max(abs(lam - lo), abs(lam - hi)) / lam < 1e-6   # |λ - λ_true| / λ bound
+    # and against the committed CPU Perron root of the same matrix
+    pin = large_pin(n, "f64")
+    assert abs(lam - pin["lambda"]) / pin["lambda"] < 1e-6
+    assert pin["cw_lo"] <= hi and lo <= pin["cw_hi"]            # brackets overlap
     # homogeneity over a fixed number of rounds: every quantity of the
     # iteration on 2A is exactly twice (s, λ) or equal to (v, D^-1 A D
     # ratios) that on A, bit for bit
@@ -507,10 +511,12 @@ def test_config4_size_on_one_gpu(solver):
     exercises every 64-bit index path), on one GPU: converges, residual
     small, matrix-free agrees, and the 32 GiB row-block path with P = 1."""
     n = 65536
-    a = dev.generate("random", n, torch.float64, seed=4, device=DEV)
+    a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
     lam_mf, v_mf, it_mf, _ = solver.solve(a, matrix_free=True)
     r = torch.mv(a, v_mf) - lam_mf * v_mf
     assert (r.abs().max() / (lam_mf * v_mf.abs().max())).item() < 1e-9
+    pin = large_pin(n, "f64")                                  # CPU Perron root
+    assert abs(lam_mf - pin["lambda"]) / pin["lambda"] < 1e-6
     lam, v, it, _ = solver.solve(a, inplace=True)
     assert it == it_mf and abs(lam - lam_mf) <= 1e-12 * lam
     assert (v - v_mf).abs().max().item() <= 1e-12
@@ -662,6 +668,10 @@ def test_config5_fp32_32768_tracks_fp64(solver):
     assert it32 == it64 == 8
     assert abs(lam32 - lam64) <= 1e-6 * lam64
     assert (v32.double() - v64).abs().max().item() <= 1e-5
+    # each against the CPU Perron root of its own generated matrix
+    for lam_, dt in ((lam32, "f32"), (lam64, "f64")):
+        pin = large_pin(n, dt)
+        assert abs(lam_ - pin["lambda"]) / pin["lambda"] < 1e-6, dt
 
 
 def test_cpp_kernel_tests():

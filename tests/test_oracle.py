@@ -149,3 +149,25 @@ def test_random_fp64_meets_north_star_accuracy(orc):
     r = orc.similarity_transform(mat, orc.SEM_SYCL)
     true = np.max(np.linalg.eigvals(mat).real)
     assert abs(r.eigen_val - true) / true < 1e-6
+
+
+def test_large_pins(orc):
+    """tests/golden/large_pins.json: CPU Perron roots of the full-size
+    BASELINE random matrices (SURVEY.md §8c large-N reference).  The
+    Collatz–Wielandt brackets are tight, λ sits near N/2 (U(0,1] entries),
+    and the C generator the pins were computed from reproduces the numpy
+    generator bit for bit on sampled rows of those very matrices."""
+    import ctypes
+
+    from conftest import large_pin
+    for n, dt in ((32768, "f64"), (32768, "f32"), (65536, "f64")):
+        p = large_pin(n, dt)
+        assert p["cw_lo"] <= p["lambda"] <= p["cw_hi"]
+        assert p["cw_rel_width"] < 1e-13
+        assert abs(p["lambda"] / (n / 2) - 1) < 1e-3
+        npdt = np.float64 if dt == "f64" else np.float32
+        for row0 in (0, n // 2 + 1, n - 1):
+            c = np.empty((1, n), npdt)
+            getattr(orc.lib(), f"orc_random_{dt}")(c.ctypes.data_as(ctypes.c_void_p), 1, n, row0, 0)
+            ref = orc.random_matrix(n, 0, npdt, nrows=1, row0=row0)
+            assert np.array_equal(c, ref)
