@@ -126,32 +126,39 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     the launch stream (torch's current stream, which the C-ABI launches on).
     At N = 1 the timed region holds nothing but the round launches, so two
     events bracket it (per-launch events would add ~7 us of event work to
-    every 175 us round); with N > 1 the all-gathers sit between launches, so
-    each launch is bracketed by its own pair."""
+    every 175 us round).  With N > 1 the all-gathers sit between launches:
+    the timed region runs without events, and a separate pass after it
+    brackets each launch with its own pair for the kernel average."""
     sh.start()
     for _ in range(warmup):
         sh.round(0.0, 2**31)
     torch.cuda.synchronize()
-    per_launch = world > 1
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(steps if per_launch else 1)]
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    if not per_launch:
+    if world == 1:
         ev[0][0].record()
     for k in range(steps):
-        sh.round(0.0, 2**31, events=ev[k] if per_launch else None)
-    if not per_launch:
+        sh.round(0.0, 2**31)
+    if world == 1:
         ev[0][1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    fused = sum(a.elapsed_time(b) for a, b in ev) / steps
-    if world > 1:
+    if world == 1:
+        fused = ev[0][0].elapsed_time(ev[0][1]) / steps
+    else:  # kernel-only average, outside the timed region
+        n_ev = min(steps, 50)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(n_ev)]
+        for k in range(n_ev):
+            sh.round(0.0, 2**31, events=ev[k])
+        torch.cuda.synchronize()
+        fused = sum(a.elapsed_time(b) for a, b in ev) / n_ev
         t = torch.tensor([el, fused], dtype=torch.float64,
                          device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
