@@ -238,7 +238,8 @@ def main():
                 "kernel": "k_round (fused stats + scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
                 "timing": ("HIP events bracketing the K timed launches on the launch stream"
-                           if world == 1 else "HIP events around every timed launch"),
+                           if world == 1 else
+                           "HIP events around every launch of a 50-round pass after the timed region"),
                 "traffic_source": None if traffic is None else traffic[1]}
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----

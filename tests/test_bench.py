@@ -1,0 +1,62 @@
+"""bench.py: the driver's JSON contract (GPU) and its host-side helpers (CPU)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+import bench  # noqa: E402
+
+
+def test_weak_scaled_sizes():
+    # per-GPU bytes stay ~constant: n = 8192*sqrt(P) rounded to 64*P
+    assert bench.scaled_n(8192, 1) == 8192
+    for p, n in ((2, 11648), (4, 16384), (8, 23040)):
+        got = bench.scaled_n(8192, p)
+        assert got == n and got % (64 * p) == 0
+        assert abs((got / p) * got / 8192**2 - 1) < 0.02
+
+
+def test_committed_measurements_are_found():
+    tr = bench.load_traffic("hilbert8192_f64")
+    assert tr is not None and abs(tr[0] / (2 * 8192**2 * 8) - 1) < 0.01
+    tr = bench.load_traffic("random32768_f64", "k_mfree")
+    assert tr is not None and abs(tr[0] / (32768**2 * 8) - 1) < 0.01
+    assert bench.load_traffic("no_such_workload") is None
+    lam = bench.true_lambda(32768, "f64", 0)
+    assert lam is not None and abs(lam / 16384 - 1) < 1e-3
+    assert bench.true_lambda(3, "f64", 0) is None
+
+
+@pytest.mark.gpu
+def test_bench_json_contract():
+    out = subprocess.run(
+        [sys.executable, os.path.join(REPO, "bench.py"), "--steps", "5", "--warmup", "1",
+         "--no-north-star", "--no-headline", "--cpu-seconds", "0.5"],
+        capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 5 and d["warmup"] == 1
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert d["dtype"] == "f64" and d["config"]["workload"] == "hilbert8192_f64"
+    r = d["roofline"]
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic"):
+        assert k in r, k
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    c = d["cpu_baseline"]
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in c, k
+    assert c["kind"] in ("port", "reference") and c["value"] > 0
+    # the reference-semantics solve inside the bench converged as published
+    assert d["solve"]["iter_count"] == 17
