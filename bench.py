@@ -257,6 +257,7 @@ def main():
                    "frac": round(by_mf_local / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                    "bytes_per_round": 1.0 * n * n * b, "solve_iter_count": it_mf,
                    "eigen_val": lam_mf}
+    mf.close()
     del mf
 
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
@@ -272,6 +273,7 @@ def main():
                                           f"row-block sharding over {world} GPU(s), "
                                           + ("strong" if args.strong else "weak") + "-scaled")},
            "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
+    sh.close()
     del sh
     torch.cuda.empty_cache()
 

@@ -193,6 +193,20 @@ class ShardedSimilarityTransform:
                 warnings.warn(f"library RCCL communicator unavailable ({e}); "
                               "using torch.distributed all_gather_into_tensor")
 
+    def close(self) -> None:
+        """Release the library's RCCL communicator (after the stream drained;
+        call on every rank)."""
+        if self.rccl is not None:
+            self.torch.cuda.synchronize()
+            self.rccl.close()
+            self.rccl = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
     # local slot of a gathered vector
     def _slot(self, s):
         p = self.part
