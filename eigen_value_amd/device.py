@@ -189,11 +189,19 @@ class DeviceSolver:
         ``mat`` is transformed in place when ``inplace`` (it is the private
         working copy the reference makes, similarity_transform.cpp:14,19).
         ``matrix_free`` runs the read-only form: the
-        input is never written, so no copy is made."""
+        input is never written, so no copy is made.  ``mat`` may be a torch
+        tensor or any DLPack producer (``__dlpack__``) on this device."""
         torch = _torch()
+        if not isinstance(mat, torch.Tensor) and hasattr(mat, "__dlpack__"):
+            mat = torch.from_dlpack(mat)   # any DLPack producer, zero copy
         _check_cuda(mat)
+        if mat.device.index != (self.device.index if self.device.index is not None
+                                else torch.cuda.current_device()):
+            raise ValueError(f"matrix on {mat.device}, solver context on {self.device}")
         n = mat.shape[0]
-        assert mat.shape == (n, n), "must be square"
+        assert mat.dim() == 2 and mat.shape == (n, n), "must be square"
+        if inplace and not mat.is_contiguous():
+            raise ValueError("inplace needs a contiguous (row-major) matrix")
         work = mat if (inplace or matrix_free) else mat.clone()
         work = work.contiguous()
         v = torch.empty(n, dtype=mat.dtype, device=mat.device)

@@ -360,6 +360,20 @@ def test_device_solver(solver, orc):
     assert np.max(np.abs(to_np(v) - ref.eigen_vec)) <= 1e-10
     lam2, v2, itr2, _ = solver.solve(a, inplace=True)
     assert lam2 == lam and torch.equal(v2, v)
+    # any DLPack producer on the device, zero copy
+    class Producer:
+        def __init__(self, t):
+            self.t = t
+
+        def __dlpack__(self, **kw):
+            return self.t.__dlpack__(**kw)
+
+        def __dlpack_device__(self):
+            return self.t.__dlpack_device__()
+    lam3, v3, itr3, _ = solver.solve(Producer(keep.clone()))
+    assert lam3 == lam and torch.equal(v3, v) and itr3 == itr
+    with pytest.raises(ValueError):
+        solver.solve(keep.t(), inplace=True)                  # non-contiguous in place
 
 
 def test_large_random_vs_oracle(solver, orc):
