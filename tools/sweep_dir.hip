@@ -90,7 +90,7 @@ struct Bufs
   st_state* st;
 };
 
-template <typename T, int ROWS, int NT, bool ALT>
+template <typename T, int ROWS, int NT, bool ALT, int U = 2>
 static void
 round_seq(const Bufs<T>& b, unsigned cap)
 {
@@ -98,13 +98,14 @@ round_seq(const Bufs<T>& b, unsigned cap)
   const unsigned ng = b.nr / ROWS;
   const unsigned grid = cap < ng ? cap : ng;
   float ms = time_seq([&](int k) {
-    hipLaunchKernelGGL((k_round<T, ROWS, W, 2, 0, NT, 256, ALT>), dim3(grid),
+    hipLaunchKernelGGL((k_round<T, ROWS, W, U, 0, NT, 256, ALT>), dim3(grid),
                        dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng, 0u, b.n, 0u,
                        (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  k_round rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s\n",
-              ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9);
+  std::printf("  k_round rows=%d nt=%d alt=%d grid=%4u  %8.4f ms  %7.1f GB/s%s\n",
+              ROWS, (int)NT, (int)ALT, grid, ms, bytes / (ms * 1e-3) / 1e9,
+              U == 2 ? "" : (U == 1 ? "  u=1" : (U == 4 ? "  u=4" : "  u=8")));
 }
 
 template <typename T, int ROWS, bool NT, bool ALT>
@@ -171,18 +172,24 @@ run(unsigned nr, unsigned n)
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
   // k_round cache policy: nt = 0 cached, 1 non-temporal loads, 2
-  // non-temporal stores, 3 both
+  // non-temporal stores, 3 both; U = chunks in flight per lane per row
+  const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
   for (unsigned cap : { 256u, 512u }) {
-    round_seq<T, 2, kNtBoth, false>(b, cap);
-    round_seq<T, 2, kCached, true>(b, cap);
-    round_seq<T, 2, kNtLoads, true>(b, cap);
-    round_seq<T, 2, kNtStores, true>(b, cap);
-    round_seq<T, 2, kNtBoth, true>(b, cap);
-    round_seq<T, 4, kNtBoth, false>(b, cap);
-    round_seq<T, 4, kCached, true>(b, cap);
-    round_seq<T, 4, kNtLoads, true>(b, cap);
-    round_seq<T, 4, kNtStores, true>(b, cap);
-    round_seq<T, 4, kNtBoth, true>(b, cap);
+    if (big) {
+      round_seq<T, 1, kNtBoth, true, 4>(b, cap);
+      round_seq<T, 2, kNtBoth, true>(b, cap);
+      round_seq<T, 2, kNtBoth, true, 4>(b, cap);
+      round_seq<T, 4, kNtBoth, true>(b, cap);
+      round_seq<T, 4, kNtBoth, true, 1>(b, cap);
+    } else {
+      round_seq<T, 1, kCached, true, 2>(b, cap);
+      round_seq<T, 1, kCached, true, 4>(b, cap);
+      round_seq<T, 1, kCached, true, 8>(b, cap);
+      round_seq<T, 2, kCached, true>(b, cap);
+      round_seq<T, 2, kCached, true, 4>(b, cap);
+      round_seq<T, 4, kCached, true>(b, cap);
+      round_seq<T, 4, kCached, true, 1>(b, cap);
+    }
   }
   for (unsigned cap : { 512u, 1024u, 2048u }) {
     mfree_seq<T, 2, true, false>(b, cap);
