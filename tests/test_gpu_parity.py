@@ -303,6 +303,26 @@ def test_residual_random_fp32(eigen):
         assert np.all(np.isclose(mat @ v, lam * v, atol=1e-3)), "Av = λv assertion failed !"
 
 
+@pytest.mark.parametrize("n", [32, 64, 128, 256, 512, 1024])
+def test_random_vs_numpy_eigvals(eigen, orc, n):
+    """main.py:62-70's randomized check (λ − max eig < EPS, one-sided) on the
+    HIP path, two-sided, and the north star's 1e-6 relative bound once λ
+    (≈ N/2) is large against the absolute EPS = 1e-3 stop (N >= 512; at
+    N = 32 the reference's own stop leaves 1.5e-5), and 128² Hilbert against
+    eigvalsh at the reference's EPS (≈1e-4 relative)."""
+    mat = orc.random_matrix(n, 7)
+    lam, v, ts, itr = eigen.similarity_transform(mat)
+    true = float(np.max(np.linalg.eigvals(mat).real))
+    assert abs(lam - true) < 1e-3
+    if n >= 512:
+        assert abs(lam - true) / true < 1e-6
+    if n == 128:
+        h = orc.hilbert(128)
+        lam_h = eigen.similarity_transform(h)[0]
+        true_h = float(np.max(np.linalg.eigvalsh(h)))
+        assert abs(lam_h - true_h) / true_h < 3e-4
+
+
 def test_deterministic(eigen, orc):
     mat = orc.random_matrix(2000, 4)
     a = eigen.similarity_transform(mat)
