@@ -42,6 +42,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MALL_BYTES = 256 << 20  # memory-side (Infinity) cache
 # fp64 Hilbert 8192, reference semantics (cyclic, EPS=1e-3): 17 rounds,
 # λ = 2.5999921826283514 (CPU oracle; README.md:76 publishes 17 rounds)
 HILBERT8192_F64 = (17, 2.5999921826283514)
@@ -241,6 +242,9 @@ def main():
                            if world == 1 else
                            "HIP events around every launch of a 50-round pass after the timed region"),
                 "traffic_source": None if traffic is None else traffic[1]}
+    if bytes_round_local / 2 <= 2 * MALL_BYTES:
+        roofline["note"] = ("matrix partly resident in the 256 MB memory-side cache: an "
+                            "effective rate, not an HBM-roofline claim (see north_star)")
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
