@@ -60,7 +60,7 @@ def parse():
     p.add_argument("--no-north-star", action="store_true")
     p.add_argument("--no-headline", action="store_true",
                    help="skip the fp32 whole-solve comparison with the published numbers")
-    p.add_argument("--cpu-seconds", type=float, default=10.0,
+    p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="CPU baseline sample length (rounds are calibrated to it)")
     p.add_argument("--strong", action="store_true",
                    help="keep n fixed for every N (strong scaling; e.g. configs[3]: "
