@@ -67,6 +67,11 @@ def parse():
                         "--n 65536 --kind random --strong)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
+    p.add_argument("--overlap", action="store_true",
+                   help="N > 1: time the overlapped exchange (split round, all-gather on a "
+                        "second stream) as the headline instead of an extra leg")
+    p.add_argument("--no-overlap-leg", action="store_true",
+                   help="N > 1: skip the extra overlapped-exchange leg")
     p.add_argument("--one-gpu", action="store_true",
                    help="rehearsal: every rank on cuda:0 (use with --backend gloo)")
     return p.parse_args()
@@ -195,7 +200,7 @@ def main():
     b = 8 if args.dtype == "f64" else 4
     n = args.n if args.strong else scaled_n(args.n, world)
     workload = f"{args.kind}{n}_{args.dtype}"
-    sh = sharded.ShardedSimilarityTransform(n, dt)
+    sh = sharded.ShardedSimilarityTransform(n, dt, overlap=args.overlap)
     p = sh.part
 
     # ---- reference-semantics solve to convergence (EPS = 1e-3) ----------
@@ -236,7 +241,9 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic[0],
-                "kernel": "k_round (fused stats + scale + row-sum)", "fused_ms_avg": round(fused_ms, 5),
+                "kernel": ("k_round_split local + remote (overlapped exchange)" if args.overlap
+                           else "k_round (fused stats + scale + row-sum)"),
+                "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
                 "timing": ("HIP events bracketing the K timed launches on the launch stream"
                            if world == 1 else
@@ -245,6 +252,24 @@ def main():
     if bytes_round_local / 2 <= 2 * MALL_BYTES:
         roofline["note"] = ("matrix partly resident in the 256 MB memory-side cache: an "
                             "effective rate, not an HBM-roofline claim (see north_star)")
+
+    # ---- N > 1: the same rounds with the exchange overlapped --------------
+    # (split launch: local columns while the all-gather runs on a second
+    # stream, sharded.py overlap=True); reported beside the headline
+    overlap_leg = None
+    if world > 1 and not args.overlap and not args.no_overlap_leg:
+        ov = sharded.ShardedSimilarityTransform(n, dt, overlap=True)
+        ov.load(args.kind)
+        lam_ov, _, it_ov, _ = ov.solve(eps=1e-3, max_itr=1000, batch=1)
+        ov.load(args.kind)
+        el_ov, k_ov = timed_rounds(ov, args.steps, args.warmup, torch, dist, world)
+        overlap_leg = {"ms_per_iteration": round(el_ov / args.steps * 1e3, 5),
+                       "value": round(bytes_round_total * args.steps / el_ov / 1e9, 2),
+                       "round_ms_avg": round(k_ov, 5),
+                       "solve_iter_count": it_ov,
+                       "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
+        ov.close()
+        del ov
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
@@ -277,6 +302,10 @@ def main():
                                           f"row-block sharding over {world} GPU(s), "
                                           + ("strong" if args.strong else "weak") + "-scaled")},
            "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
+    if args.overlap:
+        out["config"]["exchange"] = "overlapped (split round, all-gather on a second stream)"
+    if overlap_leg is not None:
+        out["exchange_overlap"] = overlap_leg
     sh.close()
     del sh
     torch.cuda.empty_cache()

@@ -133,8 +133,11 @@ def _declare(L: ctypes.CDLL) -> None:
                                                   u32, P, P]
         getattr(L, f"st_mfree_round_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, T, u32,
                                                         u32, u32, P, P]
+        getattr(L, f"st_round_split_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, u32,
+                                                        u32, T, u32, u32, u32, i32, P, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
-                     "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round"):
+                     "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round",
+                     "round_split"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32

@@ -250,12 +250,47 @@ constexpr int kNtLoads = 1;
 constexpr int kNtStores = 2;
 constexpr int kNtBoth = 3;
 
+// m / stop contribution of vector index q of s (columns q*W .. q*W+W-1):
+// the running max, and |s_i - s_{i+1}| < eps for the W pairs that start in
+// this vector (the last pair wraps to s[0] in the cyclic semantics)
+template <typename T, int W>
+__device__ __forceinline__ void
+stats_at(const T* __restrict__ s, const typename vec<T, W>::type& sc,
+         uint32_t q, uint32_t ncols, bool cyclic, T eps, T& mx, int& ok)
+{
+  T e[W + 1];
+  if constexpr (W == 1) {
+    e[0] = sc;
+  } else {
+#pragma unroll
+    for (int i = 0; i < W; i++)
+      e[i] = sc[i];
+  }
+  const uint32_t nxt = (q + 1) * W;
+  const bool has_next = nxt < ncols || cyclic;
+  e[W] = s[nxt < ncols ? nxt : 0];
+#pragma unroll
+  for (int i = 0; i < W; i++) {
+    mx = e[i] > mx ? e[i] : mx;
+    if (i < W - 1 || has_next) {
+      const T d = e[i] - e[i + 1];
+      ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0; // cpp:419-421
+    }
+  }
+}
+
+// which columns a row-group pass covers (SPAN) and where its row sums go
+constexpr int kSpanFull = 0;   // all columns -> s_next
+constexpr int kSpanLocal = 1;  // vector range [q0, q1) -> part
+constexpr int kSpanRemote = 2; // the rest -> s_next = part + sum
+
 template <typename T, int R, int W, int U, int ORDER, int NT, int BLK,
-          bool STATS>
+          bool STATS, int SPAN = kSpanFull>
 __device__ __forceinline__ void
 round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
             uint32_t rbase, uint32_t ncols, uint32_t row0, bool cyclic, T eps,
-            T& mx, int& ok, T (*red)[4])
+            T& mx, int& ok, T (*red)[4], T* __restrict__ part = nullptr,
+            uint32_t q0 = 0, uint32_t q1 = 0)
 {
   using V = typename vec<T, W>::type;
   const uint32_t nv = ncols / W;
@@ -283,28 +318,8 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
       sc[u] = sv[c + u * BLK];
     if constexpr (STATS) {
 #pragma unroll
-      for (int u = 0; u < UU; u++) {
-        const uint32_t q = c + u * BLK; // vector index: columns q*W ..
-        T e[W + 1];
-        if constexpr (W == 1) {
-          e[0] = sc[u];
-        } else {
-#pragma unroll
-          for (int i = 0; i < W; i++)
-            e[i] = sc[u][i];
-        }
-        const uint32_t nxt = (q + 1) * W;
-        const bool has_next = nxt < ncols || cyclic;
-        e[W] = s_cur[nxt < ncols ? nxt : 0];
-#pragma unroll
-        for (int i = 0; i < W; i++) {
-          mx = e[i] > mx ? e[i] : mx;
-          if (i < W - 1 || has_next) {
-            const T d = e[i] - e[i + 1];
-            ok &= (d < (T)0 ? -d : d) < eps ? 1 : 0; // cpp:419-421
-          }
-        }
-      }
+      for (int u = 0; u < UU; u++)
+        stats_at<T, W>(s_cur, sc[u], c + u * BLK, ncols, cyclic, eps, mx, ok);
     }
 #pragma unroll
     for (int u = 0; u < UU; u++)
@@ -326,12 +341,23 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
       for (int j = 0; j < R; j++)
         acc[j] += hsum<T, W>(x[u][j]);
   };
-  uint32_t c = threadIdx.x;
-  for (; c + (U - 1) * BLK < nv; c += U * BLK)
-    body(c, std::integral_constant<int, U>{});
-  if constexpr (U > 1)
-    for (; c < nv; c += BLK)
-      body(c, std::integral_constant<int, 1>{});
+  // per-lane sweep of the vector range [lo, hi) in column order
+  auto span = [&](uint32_t lo, uint32_t hi) {
+    uint32_t c = lo + threadIdx.x;
+    for (; c + (U - 1) * BLK < hi; c += U * BLK)
+      body(c, std::integral_constant<int, U>{});
+    if constexpr (U > 1)
+      for (; c < hi; c += BLK)
+        body(c, std::integral_constant<int, 1>{});
+  };
+  if constexpr (SPAN == kSpanFull) {
+    span(0, nv);
+  } else if constexpr (SPAN == kSpanLocal) {
+    span(q0, q1);
+  } else {
+    span(0, q0);
+    span(q1, nv);
+  }
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -347,18 +373,24 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 #pragma unroll
     for (int w = 1; w < BLK / 64; w++)
       t += red[w][threadIdx.x];
-    s_next[rbase + threadIdx.x] = t;
+    if constexpr (SPAN == kSpanFull)
+      s_next[rbase + threadIdx.x] = t;
+    else if constexpr (SPAN == kSpanLocal)
+      part[rbase + threadIdx.x] = t;
+    else
+      s_next[rbase + threadIdx.x] = part[rbase + threadIdx.x] + t;
   }
   __syncthreads();
 }
 
-template <typename T, int ROWS, int W, int U, int ORDER, int NT,
-          int BLK = kBlock, bool ALT = false>
-__global__ __launch_bounds__(BLK) void
-k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
-        T* __restrict__ v, uint32_t ng_main, uint32_t nrem, uint32_t ncols,
-        uint32_t row0, T eps, uint32_t k, uint32_t max_itr,
-        uint32_t semantics, st_state* state)
+template <typename T, int ROWS, int W, int U, int ORDER, int NT, int BLK,
+          bool ALT, int SPAN>
+__device__ __forceinline__ void
+round_body(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+           T* __restrict__ v, uint32_t ng_main, uint32_t nrem, uint32_t ncols,
+           uint32_t row0, T eps, uint32_t k, uint32_t max_itr,
+           uint32_t semantics, st_state* state, T* __restrict__ part,
+           uint32_t q0, uint32_t q1)
 {
   static_assert(ROWS <= 4, "red[] holds 4 rows");
   {
@@ -370,6 +402,7 @@ k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
   __shared__ T red[BLK / 64][4];
   __shared__ T mx_sh[BLK / 64];
   __shared__ T m_sh;
+  constexpr bool kStats = SPAN != kSpanLocal; // the local half only scales
   const bool cyclic = semantics == ST_SEM_SYCL;
   const uint32_t ngroups = ng_main + nrem;
   T mx = (T)0; // find_max starts from 0 (cpp:185)
@@ -385,66 +418,120 @@ k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   const bool rev = ALT && (k & 1u);
   for (uint32_t i = 0; i < cnt; i++) {
-    const bool first = i == 0;
+    const bool first = kStats && i == 0;
     const uint32_t g = blockIdx.x + (rev ? cnt - 1 - i : i) * gridDim.x;
     if (g < ng_main) {
       if (first)
-        round_group<T, ROWS, W, U, ORDER, NT, BLK, true>(
-          a, s_cur, s_next, g * ROWS, ncols, row0, cyclic, eps, mx, ok, red);
+        round_group<T, ROWS, W, U, ORDER, NT, BLK, kStats, SPAN>(
+          a, s_cur, s_next, g * ROWS, ncols, row0, cyclic, eps, mx, ok, red,
+          part, q0, q1);
       else
-        round_group<T, ROWS, W, U, ORDER, NT, BLK, false>(
+        round_group<T, ROWS, W, U, ORDER, NT, BLK, false, SPAN>(
           a, s_cur, s_next, g * ROWS, ncols, row0, cyclic, eps, dummy_mx,
-          dummy_ok, red);
+          dummy_ok, red, part, q0, q1);
     } else {
       const uint32_t rb = ng_main * ROWS + (g - ng_main);
       if (first)
-        round_group<T, 1, W, U, ORDER, NT, BLK, true>(
-          a, s_cur, s_next, rb, ncols, row0, cyclic, eps, mx, ok, red);
+        round_group<T, 1, W, U, ORDER, NT, BLK, kStats, SPAN>(
+          a, s_cur, s_next, rb, ncols, row0, cyclic, eps, mx, ok, red, part,
+          q0, q1);
       else
-        round_group<T, 1, W, U, ORDER, NT, BLK, false>(
+        round_group<T, 1, W, U, ORDER, NT, BLK, false, SPAN>(
           a, s_cur, s_next, rb, ncols, row0, cyclic, eps, dummy_mx, dummy_ok,
-          red);
+          red, part, q0, q1);
     }
   }
+  if constexpr (SPAN == kSpanLocal) {
+    return;
+  } else {
+    if constexpr (SPAN == kSpanRemote) {
+      // the remote sweep skipped the local vector range: add its m / stop
+      using V = typename vec<T, W>::type;
+      const V* sv = reinterpret_cast<const V*>(s_cur);
+      for (uint32_t q = q0 + threadIdx.x; q < q1; q += BLK)
+        stats_at<T, W>(s_cur, sv[q], q, ncols, cyclic, eps, mx, ok);
+    }
 
-  // m_k and stop_k over the whole vector (this workgroup's copy)
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0)
-    mx_sh[threadIdx.x >> 6] = mx;
-  const int stop = __syncthreads_and(ok);
-  if (threadIdx.x == 0) {
-    T m = mx_sh[0];
+    // m_k and stop_k over the whole vector (this workgroup's copy)
+    mx = wave_max(mx);
+    if ((threadIdx.x & 63) == 0)
+      mx_sh[threadIdx.x >> 6] = mx;
+    const int stop = __syncthreads_and(ok);
+    if (threadIdx.x == 0) {
+      T m = mx_sh[0];
 #pragma unroll
-    for (int w = 1; w < BLK / 64; w++)
-      m = mx_sh[w] > m ? mx_sh[w] : m;
-    m_sh = m;
-  }
-  __syncthreads();
-  const T m = m_sh;
-  // v[r] *= s_k[r] / m_k for this workgroup's rows (cpp:260)
-  for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
-    const uint32_t rb = g < ng_main ? g * ROWS : ng_main * ROWS + (g - ng_main);
-    const uint32_t nr = g < ng_main ? ROWS : 1;
-    if (threadIdx.x < nr) {
-      const uint32_t r = row0 + rb + threadIdx.x;
-      v[r] = v[r] * (s_cur[r] / m);
+      for (int w = 1; w < BLK / 64; w++)
+        m = mx_sh[w] > m ? mx_sh[w] : m;
+      m_sh = m;
+    }
+    __syncthreads();
+    const T m = m_sh;
+    // v[r] *= s_k[r] / m_k for this workgroup's rows (cpp:260)
+    for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+      const uint32_t rb =
+        g < ng_main ? g * ROWS : ng_main * ROWS + (g - ng_main);
+      const uint32_t nr = g < ng_main ? ROWS : 1;
+      if (threadIdx.x < nr) {
+        const uint32_t r = row0 + rb + threadIdx.x;
+        v[r] = v[r] * (s_cur[r] / m);
+      }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      state->lambda = (double)s_cur[0]; // cpp:60-65
+      state->max = (double)m;
+      state->stop = stop ? 1u : 0u;
+      state->round = k;
+      if (stop) {
+        state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
+        state->end = k + 1;
+        state->done = 1u;
+      } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
+        state->iters = max_itr;
+        state->end = k + 1;
+        state->done = 1u;
+      }
     }
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    state->lambda = (double)s_cur[0]; // cpp:60-65
-    state->max = (double)m;
-    state->stop = stop ? 1u : 0u;
-    state->round = k;
-    if (stop) {
-      state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
-      state->end = k + 1;
-      state->done = 1u;
-    } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
-      state->iters = max_itr;
-      state->end = k + 1;
-      state->done = 1u;
-    }
-  }
+}
+
+template <typename T, int ROWS, int W, int U, int ORDER, int NT,
+          int BLK = kBlock, bool ALT = false>
+__global__ __launch_bounds__(BLK) void
+k_round(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+        T* __restrict__ v, uint32_t ng_main, uint32_t nrem, uint32_t ncols,
+        uint32_t row0, T eps, uint32_t k, uint32_t max_itr,
+        uint32_t semantics, st_state* state)
+{
+  round_body<T, ROWS, W, U, ORDER, NT, BLK, ALT, kSpanFull>(
+    a, s_cur, s_next, v, ng_main, nrem, ncols, row0, eps, k, max_itr,
+    semantics, state, nullptr, 0u, 0u);
+}
+
+// ---------------------------------------------------------------------------
+// the round split in two launches, for a sharded solve whose all-gather of
+// s_k overlaps the first (sharded.py, overlap=True).  Rank p owns rows
+// [row0, row0 + nrows) and therefore computed s_k for exactly the matching
+// columns, vector range [q0, q1):
+//   SPAN = kSpanLocal  (before the gather completes): those columns only —
+//     A[r][c] *= s_k[c] / s_k[r], part[r] = their row sums; no stats
+//   SPAN = kSpanRemote (after it): m_k / stop_k over the full s_k, the v
+//     update, the remaining columns, s_{k+1}[r] = part[r] + their sum
+// Element updates, m, stop and v are bit-identical to k_round; s_{k+1} adds
+// the two column sets separately (fixed order, so still deterministic; for
+// P = 1 the remote set is empty and s_{k+1} equals k_round's bit for bit).
+// ---------------------------------------------------------------------------
+template <typename T, int ROWS, int W, int U, int ORDER, int NT, int SPAN,
+          int BLK = kBlock, bool ALT = true>
+__global__ __launch_bounds__(BLK) void
+k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
+              T* __restrict__ part, T* __restrict__ v, uint32_t ng_main,
+              uint32_t nrem, uint32_t ncols, uint32_t row0, uint32_t q0,
+              uint32_t q1, T eps, uint32_t k, uint32_t max_itr,
+              uint32_t semantics, st_state* state)
+{
+  round_body<T, ROWS, W, U, ORDER, NT, BLK, ALT, SPAN>(
+    a, s_cur, s_next, v, ng_main, nrem, ncols, row0, eps, k, max_itr,
+    semantics, state, part, q0, q1);
 }
 
 // ---------------------------------------------------------------------------

@@ -208,6 +208,65 @@ launch_round_rows(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
 #undef ST_ROUND_CFG
 }
 
+template <typename T, int ROWS, int W, int ORDER, int NT, int SPAN>
+void
+launch_split_cfg(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                 uint32_t nrows, uint32_t ncols, uint32_t row0, uint32_t q0,
+                 uint32_t q1, T eps, uint32_t k, uint32_t max_itr,
+                 uint32_t semantics, st_state* st, uint32_t cap,
+                 hipStream_t stream)
+{
+  const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
+  const uint32_t ng = ng_main + nrem;
+  const uint32_t grid = ng < cap ? ng : cap;
+  hipLaunchKernelGGL((dev::k_round_split<T, ROWS, W, kUnroll, ORDER, NT, SPAN>),
+                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, s_next,
+                     part, v, ng_main, nrem, ncols, row0, q0, q1, eps, k,
+                     max_itr, semantics, st);
+}
+
+template <typename T, int W, int ORDER, int SPAN>
+void
+launch_split_rows(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                  uint32_t nrows, uint32_t ncols, uint32_t row0, uint32_t q0,
+                  uint32_t q1, T eps, uint32_t k, uint32_t max_itr,
+                  uint32_t semantics, st_state* st, hipStream_t stream)
+{
+  // the shape of the whole round (both halves stream the same rows)
+  const Shape sh = round_shape(nrows, ncols, sizeof(T));
+#define ST_SPLIT_CFG(R, N)                                                     \
+  launch_split_cfg<T, R, W, ORDER, N, SPAN>(a, s_cur, s_next, part, v, nrows,  \
+                                            ncols, row0, q0, q1, eps, k,       \
+                                            max_itr, semantics, st, sh.grid,   \
+                                            stream)
+  using dev::kCached;
+  using dev::kNtBoth;
+  if (sh.rows == 1)
+    ST_SPLIT_CFG(1, kCached);
+  else if (sh.rows == 2)
+    sh.nt ? ST_SPLIT_CFG(2, kNtBoth) : ST_SPLIT_CFG(2, kCached);
+  else
+    sh.nt ? ST_SPLIT_CFG(4, kNtBoth) : ST_SPLIT_CFG(4, kCached);
+#undef ST_SPLIT_CFG
+}
+
+template <typename T, int W, int SPAN>
+void
+launch_split_order(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                   uint32_t nrows, uint32_t ncols, uint32_t row0, uint32_t q0,
+                   uint32_t q1, T eps, uint32_t k, uint32_t max_itr,
+                   uint32_t semantics, st_state* st, hipStream_t stream)
+{
+  if (semantics == ST_SEM_MAINPY)
+    launch_split_rows<T, W, 1, SPAN>(a, s_cur, s_next, part, v, nrows, ncols,
+                                     row0, q0, q1, eps, k, max_itr, semantics,
+                                     st, stream);
+  else
+    launch_split_rows<T, W, 0, SPAN>(a, s_cur, s_next, part, v, nrows, ncols,
+                                     row0, q0, q1, eps, k, max_itr, semantics,
+                                     st, stream);
+}
+
 template <typename T, int ROWS, int W, bool NT>
 void
 launch_mfree_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
@@ -306,6 +365,41 @@ launch_round(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                                  k, max_itr, semantics, st, stream);
   }
   return check_launch("round");
+}
+
+template <typename T>
+int
+launch_round_split(int span, T* a, const T* s_cur, T* s_next, T* part, T* v,
+                   uint32_t nrows, uint32_t ncols, uint32_t row0,
+                   uint32_t col0, uint32_t col1, T eps, uint32_t k,
+                   uint32_t max_itr, uint32_t semantics, st_state* st,
+                   hipStream_t stream)
+{
+  ST_REQUIRE(a && s_cur && part && st, "round_split: null pointer");
+  ST_REQUIRE(span == 1 || span == 2, "round_split: span must be 1 (local) "
+                                     "or 2 (remote), not %d", span);
+  ST_REQUIRE(span == 1 || (s_next && v), "round_split: null pointer");
+  ST_REQUIRE(ncols > 0 && nrows > 0, "round_split: empty block");
+  ST_REQUIRE(col0 <= col1 && col1 <= ncols,
+             "round_split: bad local column range [%u, %u) of %u", col0, col1,
+             ncols);
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "round_split: bad semantics %u",
+             semantics);
+  ST_REQUIRE(max_itr > 0, "round_split: max_itr must be > 0");
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && (col0 % W) == 0 && (col1 % W) == 0 &&
+                      aligned16(a) && aligned16(s_cur);
+  const uint32_t w = vec_ok ? W : 1;
+  const uint32_t q0 = col0 / w, q1 = col1 / w;
+#define ST_SPLIT(WW, SP)                                                       \
+  launch_split_order<T, WW, SP>(a, s_cur, s_next, part, v, nrows, ncols, row0, \
+                                q0, q1, eps, k, max_itr, semantics, st, stream)
+  if (vec_ok)
+    span == 1 ? ST_SPLIT(W, dev::kSpanLocal) : ST_SPLIT(W, dev::kSpanRemote);
+  else
+    span == 1 ? ST_SPLIT(1, dev::kSpanLocal) : ST_SPLIT(1, dev::kSpanRemote);
+#undef ST_SPLIT
+  return check_launch("round_split");
 }
 
 template <typename T>
@@ -505,6 +599,20 @@ st_state_reset(st_state* d_state, void* stream)
     return st::launch_round<T>(d_mat, d_s_cur, d_s_next, d_v, nrows, ncols,    \
                                row0, eps, k, max_itr, semantics, d_state,      \
                                ST_STREAM(stream));                             \
+  }                                                                            \
+  int st_round_split_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,           \
+                           T* d_part, T* d_v, unsigned int nrows,              \
+                           unsigned int ncols, unsigned int row0,              \
+                           unsigned int col0, unsigned int col1, T eps,        \
+                           unsigned int k, unsigned int max_itr,               \
+                           unsigned int semantics, int span,                   \
+                           st_state* d_state, void* stream)                    \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_round_split<T>(span, d_mat, d_s_cur, d_s_next, d_part,   \
+                                     d_v, nrows, ncols, row0, col0, col1, eps, \
+                                     k, max_itr, semantics, d_state,           \
+                                     ST_STREAM(stream));                       \
   }                                                                            \
   int st_mfree_round_##SFX(const T* d_mat0, const T* d_s_prev, T* d_s_next,    \
                            const T* d_v_prev, T* d_v_cur, unsigned int nrows,  \

@@ -156,6 +156,30 @@ def mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0: int = 0,
         row0, eps, k, max_itr, semantics, _ptr(state), _stream(mat0.device)), "mfree_round")
 
 
+SPAN_LOCAL = 1
+SPAN_REMOTE = 2
+
+
+def split_round(mat, s_cur, s_next, part, v, state, *, span: int, row0: int = 0,
+                col0: int = 0, col1: Optional[int] = None, eps: float = 0.0, k: int = 0,
+                max_itr: int = _lib.ST_MAX_ITR, semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """Half of a round (st_round_split): ``span=SPAN_LOCAL`` transforms the
+    columns [col0, col1) and writes their row sums to ``part``;
+    ``span=SPAN_REMOTE`` does the rest of the round (m/stop/v/state from
+    the full ``s_cur``, the other columns, ``s_next = part + their sum``)."""
+    _check_cuda(mat, s_cur, s_next, part, v, state)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    col1 = ncols if col1 is None else col1
+    assert s_cur.numel() >= ncols and part.numel() >= nrows and row0 + nrows <= ncols
+    assert span == SPAN_LOCAL or (s_next is not None and s_next.numel() >= nrows
+                                  and v is not None and v.numel() >= ncols)
+    _lib.check(getattr(_lib.load(), f"st_round_split_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(s_next), _ptr(part), _ptr(v), nrows, ncols, row0,
+        col0, col1, eps, k, max_itr, semantics, span, _ptr(state),
+        _stream(mat.device)), "round_split")
+
+
 def epilogue(s, v, state, eps: float, max_itr: int = _lib.ST_MAX_ITR,
              semantics: int = _lib.ST_SEM_SYCL) -> None:
     """Round epilogue: max, v *= s/m, stop test, λ = s[0], bookkeeping."""

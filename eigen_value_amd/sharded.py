@@ -14,6 +14,15 @@ owns the contiguous rows ``[p*chunk, p*chunk + nrows_p)`` of A, with
 
 At the end one more all-gather assembles the eigenvector slices.
 
+``overlap=True`` (transform form) hides the all-gather behind compute: the
+round is split into two launches (``st_round_split_*``).  The columns whose
+scales a rank computed itself need no exchange, so while the all-gather of
+s_k runs on a communication stream the rank already transforms its
+[row0, row0 + nrows) column block; the second launch, after the gather,
+does the stats, the eigenvector update and the remaining columns.  A, v, m
+and the stop decisions are bit-identical to the one-launch round; s_{k+1}
+sums the two column sets separately (deterministic, bit-identical at P = 1).
+
 The reference has no distributed code at all ("Parallelism
 strategies ... none"); this is the exchange north_star asks for.  The
 per-shard compute is pluggable (``ops``): ``HipShardOps`` runs the HIP
@@ -89,6 +98,17 @@ class HipShardOps:
         self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
                        max_itr=max_itr, semantics=semantics, state=state)
 
+    def split_round(self, mat, s_cur, s_next, part, v, row0, col0, col1, eps, k, max_itr,
+                    semantics, state, span):
+        self.dev.split_round(mat, s_cur, s_next, part, v, state, span=span, row0=row0,
+                             col0=col0, col1=col1, eps=eps, k=k, max_itr=max_itr,
+                             semantics=semantics)
+
+    def make_streams(self):
+        """(communication stream, 's_k slot ready' event, 'gathered' event)."""
+        torch = self.torch
+        return (torch.cuda.Stream(self.device), torch.cuda.Event(), torch.cuda.Event())
+
     def mfree_round(self, mat0, s_prev, s_next, v_prev, v_cur, row0, eps, k, max_itr,
                     semantics, state):
         self.dev.mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0=row0,
@@ -154,7 +174,7 @@ class ShardedSimilarityTransform:
 
     def __init__(self, n: int, dtype=None, group=None, ops=None,
                  semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False,
-                 comm: str = "auto"):
+                 comm: str = "auto", overlap: bool = False):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -174,6 +194,14 @@ class ShardedSimilarityTransform:
                    for _ in range(2 if matrix_free else 1)]
         self.v = self.vb[0]
         self.state = self.ops.new_state()
+        if overlap and matrix_free:
+            raise ValueError("overlap applies to the transform form only")
+        self.overlap = overlap
+        self.part_sums = self.ops.empty((p.chunk,), self.dtype) if overlap else None
+        # device ops overlap on a second stream; the CPU test double runs
+        # the same calls in program order
+        self._streams = (self.ops.make_streams()
+                         if overlap and hasattr(self.ops, "make_streams") else None)
         self.mat = None
         self.k = 0
         self.cur = 0
@@ -237,7 +265,8 @@ class ShardedSimilarityTransform:
         self.ops.reset_state(self.state)
         self.ops.fill(self.v, 1.0)
         self.ops.rowsum(self.mat, self._slot(self.s[0]))
-        self.gather(self.s[0])
+        if not self.overlap:          # the overlapped round 0 gathers s_0 itself
+            self.gather(self.s[0])
         self.cur = 0
         self.k = 0
 
@@ -246,6 +275,8 @@ class ShardedSimilarityTransform:
         s_{k+1}) then the all-gather of s_{k+1}.  Matrix-free: launch k+1
         (round k's stats and v_k over the full vector, s_{k+1} = (A_0 x) ⊘ x
         for the local rows) then the same all-gather."""
+        if self.overlap:
+            return self._round_overlap(eps, max_itr, events)
         p, cur, k = self.part, self.cur, self.k
         if events is not None:
             events[0].record()
@@ -259,6 +290,38 @@ class ShardedSimilarityTransform:
         if events is not None:
             events[1].record()
         self.gather(self.s[cur ^ 1])
+        self.cur = cur ^ 1
+        self.k += 1
+
+    def _round_overlap(self, eps: float, max_itr: int, events=None):
+        """Round k with the all-gather of s_k overlapping the local half:
+            comm stream:    wait(slot of s_k written) -> all-gather s_k
+            compute stream: local columns -> wait(gathered) -> the rest
+        """
+        p, cur, k = self.part, self.cur, self.k
+        s_k = self.s[cur][:p.n]
+        lo, hi = p.row0, p.row0 + p.nrows
+        if events is not None:
+            events[0].record()
+        if self._streams is not None:
+            torch = self.torch
+            comm, ready, gathered = self._streams
+            ready.record()
+            comm.wait_event(ready)
+            with torch.cuda.stream(comm):
+                self.gather(self.s[cur])
+                gathered.record()
+        self.ops.split_round(self.mat, s_k, None, self.part_sums, None, p.row0, lo, hi,
+                             eps, k, max_itr, self.semantics, self.state, span=1)
+        if self._streams is not None:
+            torch.cuda.current_stream().wait_event(gathered)
+        else:
+            self.gather(self.s[cur])
+        self.ops.split_round(self.mat, s_k, self._slot(self.s[cur ^ 1]), self.part_sums,
+                             self.v, p.row0, lo, hi, eps, k, max_itr, self.semantics,
+                             self.state, span=2)
+        if events is not None:
+            events[1].record()
         self.cur = cur ^ 1
         self.k += 1
 

@@ -264,6 +264,35 @@ int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                  unsigned int max_itr, unsigned int semantics,
                  st_state* d_state, void* stream);
 
+/* Round k split in two launches for a sharded solve that overlaps the
+ * all-gather of s_k with compute (eigen_value_amd/sharded.py, overlap).
+ * [col0, col1) are the columns whose s_k values this rank computed itself
+ * (normally [row0, row0 + nrows)); d_part holds nrows partial row sums.
+ *   span = 1 (local; d_s_cur needs only the own slot): for those columns
+ *     A[r][c] <- A[r][c] * ((1/s_k[row0+r]) * s_k[c]), d_part[r] = their
+ *     sum.  No m / stop / v / state work.
+ *   span = 2 (remote; d_s_cur = the full gathered s_k): exactly st_round's
+ *     m_k, stop_k, v update, lambda and state, plus the other columns, and
+ *     d_s_next[r] = d_part[r] + (their row sum).
+ * A_{k+1}, v, m and stop are bit-identical to st_round; s_{k+1} sums the
+ * two column sets separately (bit-identical to st_round when the local
+ * range is all columns).  Both launches are no-ops once a previous round
+ * stopped. */
+int st_round_split_f32(float* d_mat, const float* d_s_cur, float* d_s_next,
+                       float* d_part, float* d_v, unsigned int nrows,
+                       unsigned int ncols, unsigned int row0,
+                       unsigned int col0, unsigned int col1, float eps,
+                       unsigned int k, unsigned int max_itr,
+                       unsigned int semantics, int span, st_state* d_state,
+                       void* stream);
+int st_round_split_f64(double* d_mat, const double* d_s_cur,
+                       double* d_s_next, double* d_part, double* d_v,
+                       unsigned int nrows, unsigned int ncols,
+                       unsigned int row0, unsigned int col0,
+                       unsigned int col1, double eps, unsigned int k,
+                       unsigned int max_itr, unsigned int semantics, int span,
+                       st_state* d_state, void* stream);
+
 /* Matrix-free round.  The transformed matrix of
  * round k is X^-1 A_0 X with x ∝ the product of all previous row-sum
  * vectors, so its row sums are (A_0 x) ⊘ x and A_0 never has to be

@@ -181,6 +181,54 @@ def test_round_stop_and_gating(orc):
     assert st2["done"] == 1 and st2["stop"] == 0 and st2["iters"] == 5 and st2["end"] == 5
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("nrows,ncols,row0", [(512, 1536, 512), (1500, 1500, 0), (7, 257, 100),
+                                              (2049, 6000, 3000)])
+def test_split_round_matches_round(orc, dt, nrows, ncols, row0):
+    """st_round_split_* local + remote == st_round_*: A_{k+1}, v and the
+    state bit for bit; s_{k+1} to rounding (two column sets summed apart),
+    and bit for bit when the local set is every column."""
+    a = orc.random_matrix(ncols, 3, dt, nrows=nrows)
+    s_full = np.ascontiguousarray((orc.random_matrix(ncols, 9, dt, nrows=1)[0]
+                                   + dt(0.5)).astype(dt))
+    v0 = orc.random_matrix(ncols, 5, dt, nrows=1)[0]
+    outs = []
+    for col0, col1 in ((None, None), (row0, row0 + nrows), (0, ncols)):
+        ta, ts, tv = (torch.from_numpy(x).to(DEV) for x in (a, s_full, v0))
+        s_next = torch.empty(nrows, dtype=TD[dt], device=DEV)
+        state = dev.new_state(DEV)
+        if col0 is None:
+            dev.fused_round(ta, ts, s_next, tv, state, row0=row0, eps=1e-3, k=3)
+        else:
+            part = torch.empty(nrows, dtype=TD[dt], device=DEV)
+            dev.split_round(ta, ts, None, part, None, state, span=dev.SPAN_LOCAL, row0=row0,
+                            col0=col0, col1=col1, eps=1e-3, k=3)
+            dev.split_round(ta, ts, s_next, part, tv, state, span=dev.SPAN_REMOTE, row0=row0,
+                            col0=col0, col1=col1, eps=1e-3, k=3)
+        outs.append((to_np(ta), to_np(s_next), to_np(tv), dev.read_state(state)))
+    base = outs[0]
+    for got in outs[1:]:
+        assert np.array_equal(got[0], base[0]) and np.array_equal(got[2], base[2])
+        assert got[3] == base[3]
+        tol = 1e-14 if dt == np.float64 else 1e-6
+        assert np.max(np.abs(got[1] - base[1]) / base[1]) <= tol
+    assert np.array_equal(outs[2][1], base[1])           # local = all columns
+
+
+def test_sharded_overlap_single_gpu_bitwise(solver):
+    """overlap=True at P = 1 (streams, events and the split launches; the
+    gather is empty) gives bitwise the one-launch result."""
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+    n = 3000
+    res = []
+    for overlap in (False, True):
+        sh = ShardedSimilarityTransform(n, torch.float64, overlap=overlap)
+        sh.load("hilbert")
+        res.append(sh.solve(eps=1e-3))
+    (l0, v0, i0, r0), (l1, v1, i1, r1) = res
+    assert l0 == l1 and i0 == i1 and r0 == r1 and torch.equal(v0, v1)
+
+
 def test_sharded_single_gpu_matches_device_solver(solver):
     from eigen_value_amd.sharded import ShardedSimilarityTransform
     n = 3000
@@ -193,14 +241,14 @@ def test_sharded_single_gpu_matches_device_solver(solver):
     assert torch.equal(v, v2)
 
 
-def _gpu_gloo_worker(rank, world, port, n, outdir):
+def _gpu_gloo_worker(rank, world, port, n, outdir, overlap=False):
     import torch.distributed as dist
     from eigen_value_amd.sharded import ShardedSimilarityTransform
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sh = ShardedSimilarityTransform(n, torch.float64)
+        sh = ShardedSimilarityTransform(n, torch.float64, overlap=overlap)
         sh.load("random", seed=6)
         lam, v, iters, rounds = sh.solve(eps=1e-3)
         np.save(os.path.join(outdir, f"v{rank}.npy"), v.cpu().numpy())
@@ -226,6 +274,28 @@ def test_sharded_two_ranks_on_one_gpu(tmp_path, solver):
         lam_r, it_r, rounds_r = np.load(tmp_path / f"m{r}.npy")
         assert lam_r == lam and int(it_r) == it and int(rounds_r) == st["rounds"]
         assert np.array_equal(np.load(tmp_path / f"v{r}.npy"), to_np(v))
+
+
+def test_sharded_overlap_two_ranks_on_one_gpu(tmp_path, solver):
+    """P = 2 with the overlapped exchange (communication stream, events,
+    split launches; gloo on one GPU): same iterations and rounds as the
+    single-GPU solve, λ and v to fp64 rounding, identical on both ranks."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    n = 2502                                   # 1251 rows each (even split, odd size)
+    mp.spawn(_gpu_gloo_worker, args=(2, port, n, str(tmp_path), True), nprocs=2, join=True)
+    a = dev.generate("random", n, torch.float64, seed=6, device=DEV)
+    lam, v, it, st = solver.solve(a)
+    v0 = np.load(tmp_path / "v0.npy")
+    for r in range(2):
+        lam_r, it_r, rounds_r = np.load(tmp_path / f"m{r}.npy")
+        assert int(it_r) == it and int(rounds_r) == st["rounds"]
+        assert abs(lam_r - lam) <= 1e-13 * lam
+        vr = np.load(tmp_path / f"v{r}.npy")
+        assert np.array_equal(vr, v0) and np.max(np.abs(vr - to_np(v))) <= 1e-13
 
 
 def test_fused_step_is_gated_by_done(orc):

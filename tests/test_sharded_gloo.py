@@ -99,6 +99,35 @@ class CpuShardOps:
         mat.copy_(torch.from_numpy(new))
         s_next.copy_(torch.from_numpy(self.o.rowsum(new)))
 
+    def split_round(self, mat, s_cur, s_next, part, v, row0, col0, col1, eps, k, max_itr,
+                    semantics, st, span):
+        # the st_round_split_* contract, restated: span 1 = the [col0, col1)
+        # columns into part, span 2 = stats / v / state + the other columns
+        e = st.get("end", 0)
+        if e and e <= k:
+            return
+        sn = s_cur.numpy()
+        nr = mat.shape[0]
+        order = 0 if semantics == _lib.ST_SEM_SYCL else 1
+        new = self.o.compute_next(mat.numpy(), sn, row0=row0, order=order)
+        if span == 1:
+            mat[:, col0:col1] = torch.from_numpy(new[:, col0:col1])
+            part[:nr] = torch.from_numpy(self.o.rowsum(np.ascontiguousarray(new[:, col0:col1])))
+            return
+        m = self.o.find_max(sn)
+        vl = v[row0:row0 + nr]
+        vl.copy_(torch.from_numpy(self.o.compute_eigen_vector(sn[row0:row0 + nr], m, vl.numpy())))
+        ok = self.o.stop(sn, eps=sn.dtype.type(eps), cyclic=semantics == _lib.ST_SEM_SYCL)
+        st.update(eigen_val=float(sn[0]), max=float(m), stop=int(ok), round=k)
+        if ok:
+            st.update(done=1, end=k + 1, iters=k if semantics == _lib.ST_SEM_SYCL else k + 1)
+        elif k + 1 >= max_itr:
+            st.update(done=1, end=k + 1, iters=max_itr)
+        rest = np.ascontiguousarray(np.concatenate([new[:, :col0], new[:, col1:]], axis=1))
+        mat[:, :col0] = torch.from_numpy(new[:, :col0])
+        mat[:, col1:] = torch.from_numpy(new[:, col1:])
+        s_next.copy_(part[:nr] + torch.from_numpy(self.o.rowsum(rest)))
+
     def mfree_round(self, mat0, s_prev, s_next, v_prev, v_cur, row0, eps, k, max_itr,
                     semantics, st):
         # the st_mfree_round_* contract, restated (numpy matmul as the GEMV)
@@ -129,12 +158,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, n, kind, dtype, semantics, outdir, matrix_free=False):
+def _worker(rank, world, port, n, kind, dtype, semantics, outdir, matrix_free=False,
+            overlap=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         sh = ShardedSimilarityTransform(n, dtype, ops=CpuShardOps(), semantics=semantics,
-                                        matrix_free=matrix_free)
+                                        matrix_free=matrix_free, overlap=overlap)
         sh.load(kind, seed=3)
         lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=3)
         np.save(os.path.join(outdir, f"v{rank}.npy"), v.numpy())
@@ -193,3 +223,36 @@ def test_sharded_matrix_free_matches_oracle(tmp_path, orc, world, n):
         v = np.load(tmp_path / f"v{r}.npy")
         assert np.array_equal(v, v0)                      # identical on every rank
         assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-12
+
+
+@pytest.mark.parametrize("world,n,kind,semantics", [
+    (2, 128, "hilbert", _lib.ST_SEM_SYCL),
+    (3, 101, "random", _lib.ST_SEM_MAINPY),
+    (1, 64, "hilbert", _lib.ST_SEM_SYCL),
+])
+def test_sharded_overlap_matches_oracle(tmp_path, orc, world, n, kind, semantics):
+    """Overlapped exchange (two launches per round, the all-gather between
+    them): same rounds and iteration count as the oracle, λ and v to fp64
+    rounding (the row sums add the local and the remote column sets
+    separately); bit-identical to the oracle at P = 1 (no remote set)."""
+    mp.spawn(_worker, args=(world, _free_port(), n, kind, torch.float64, semantics,
+                            str(tmp_path), False, True), nprocs=world, join=True)
+    mat = orc.hilbert(n) if kind == "hilbert" else orc.random_matrix(n, 3)
+    ref = orc.similarity_transform(mat, semantics)
+    v0 = np.load(tmp_path / "v0.npy")
+    for r in range(world):
+        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")
+        v = np.load(tmp_path / f"v{r}.npy")
+        assert int(iters) == ref.iter_count and int(rounds) == ref.rounds_evaluated
+        assert np.array_equal(v, v0)                      # identical on every rank
+        if world == 1:
+            assert lam == ref.eigen_val and np.array_equal(v, ref.eigen_vec)
+        else:
+            assert abs(lam - ref.eigen_val) <= 1e-13 * ref.eigen_val
+            assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-13
+
+
+def test_overlap_rejects_matrix_free():
+    with pytest.raises(ValueError):
+        ShardedSimilarityTransform(64, torch.float64, ops=CpuShardOps(), matrix_free=True,
+                                   overlap=True)

@@ -48,6 +48,9 @@ for s in $STEPS; do
     multi) # the N > 1 bench path rehearsed on one GPU (gloo exchange)
       step bench_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu
       step bench_p4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 20 --warmup 3 --backend gloo --one-gpu ;;
+    overlap) # the overlapped exchange: N = 1 (split launches, empty gather) and the rehearsal
+      step bench_overlap_p1 600 python bench.py --overlap --no-cpu --no-north-star --no-headline
+      step bench_overlap_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu --overlap --no-overlap-leg ;;
     fp32)  step fp32_study 600 python3 tools/fp32_study.py --out "$OUT/fp32_study.json" ;;
     profile)
       # one workload per profiled command, so every rocprofv3 summary row
