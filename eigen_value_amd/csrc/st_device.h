@@ -414,8 +414,20 @@ round_body(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
   // so a round starts on the rows the previous round wrote last (still in
   // the memory-side cache) while each workgroup keeps the same rows (and
   // XCD) every round
-  const uint32_t cnt =
+  uint32_t cnt =
     blockIdx.x < ngroups ? (ngroups - 1 - blockIdx.x) / gridDim.x + 1 : 0;
+  if constexpr (SPAN == kSpanRemote) {
+    if (q0 == 0 && q1 == ncols / W) { // nothing remote (P = 1): s_next = part
+      for (uint32_t g = blockIdx.x; g < ngroups; g += gridDim.x) {
+        const uint32_t rb =
+          g < ng_main ? g * ROWS : ng_main * ROWS + (g - ng_main);
+        const uint32_t nr = g < ng_main ? ROWS : 1;
+        if (threadIdx.x < nr)
+          s_next[rb + threadIdx.x] = part[rb + threadIdx.x] + (T)0;
+      }
+      cnt = 0;
+    }
+  }
   const bool rev = ALT && (k & 1u);
   for (uint32_t i = 0; i < cnt; i++) {
     const bool first = kStats && i == 0;
@@ -445,10 +457,23 @@ round_body(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     return;
   } else {
     if constexpr (SPAN == kSpanRemote) {
-      // the remote sweep skipped the local vector range: add its m / stop
+      // the remote sweep skipped the local vector range: add its m / stop,
+      // 8 vectors in flight per lane (a dependent load per vector would
+      // leave this short pass latency-bound)
       using V = typename vec<T, W>::type;
       const V* sv = reinterpret_cast<const V*>(s_cur);
-      for (uint32_t q = q0 + threadIdx.x; q < q1; q += BLK)
+      constexpr int kU = 8;
+      uint32_t q = q0 + threadIdx.x;
+      for (; q + (kU - 1) * BLK < q1; q += kU * BLK) {
+        V x[kU];
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+          x[u] = sv[q + u * BLK];
+#pragma unroll
+        for (int u = 0; u < kU; u++)
+          stats_at<T, W>(s_cur, x[u], q + u * BLK, ncols, cyclic, eps, mx, ok);
+      }
+      for (; q < q1; q += BLK)
         stats_at<T, W>(s_cur, sv[q], q, ncols, cyclic, eps, mx, ok);
     }
 

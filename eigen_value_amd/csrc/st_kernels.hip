@@ -232,19 +232,23 @@ launch_split_rows(T* a, const T* s_cur, T* s_next, T* part, T* v,
                   uint32_t q1, T eps, uint32_t k, uint32_t max_itr,
                   uint32_t semantics, st_state* st, hipStream_t stream)
 {
-  // the shape of the whole round (both halves stream the same rows)
+  // the shape of the whole round (both halves stream the same rows); the
+  // local half streams non-temporally so that it does not evict what the
+  // remote half re-reads from the memory-side cache round after round
+  // (tools/sweep_dir.hip SWEEP_SPLIT=1: at the P = 8 block the pair then
+  // costs 4 us over one k_round launch instead of 25 us)
   const Shape sh = round_shape(nrows, ncols, sizeof(T));
 #define ST_SPLIT_CFG(R, N)                                                     \
-  launch_split_cfg<T, R, W, ORDER, N, SPAN>(a, s_cur, s_next, part, v, nrows,  \
-                                            ncols, row0, q0, q1, eps, k,       \
-                                            max_itr, semantics, st, sh.grid,   \
-                                            stream)
+  launch_split_cfg<T, R, W, ORDER,                                             \
+                   SPAN == dev::kSpanLocal ? dev::kNtBoth : (N), SPAN>(        \
+    a, s_cur, s_next, part, v, nrows, ncols, row0, q0, q1, eps, k, max_itr,    \
+    semantics, st, sh.grid, stream)
   using dev::kCached;
   using dev::kNtBoth;
+  // 4 rows per group whenever rows are grouped: each half sweeps only part
+  // of a row, so more rows amortise the per-group reduction (6 % at P = 8)
   if (sh.rows == 1)
     ST_SPLIT_CFG(1, kCached);
-  else if (sh.rows == 2)
-    sh.nt ? ST_SPLIT_CFG(2, kNtBoth) : ST_SPLIT_CFG(2, kCached);
   else
     sh.nt ? ST_SPLIT_CFG(4, kNtBoth) : ST_SPLIT_CFG(4, kCached);
 #undef ST_SPLIT_CFG

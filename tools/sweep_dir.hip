@@ -108,6 +108,49 @@ round_seq(const Bufs<T>& b, unsigned cap)
               U == 2 ? "" : (U == 1 ? "  u=1" : (U == 4 ? "  u=4" : "  u=8")));
 }
 
+// one launch (k_round) vs the split pair (k_round_split local + remote,
+// back to back, no exchange) on the same block: the cost of splitting the
+// round for the overlapped exchange, local columns = [c0, c0 + nr)
+template <typename T, int ROWS, int NT, int NTL = NT>
+static void
+split_seq(const Bufs<T>& b, unsigned cap, unsigned c0)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ng = b.nr / ROWS;
+  const unsigned grid = cap < ng ? cap : ng;
+  const unsigned q0 = c0 / W, q1 = (c0 + b.nr) / W;
+  float one = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round<T, ROWS, W, 2, 0, NT, 256, true>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng, 0u, b.n, c0,
+                       (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+  });
+  float loc = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round_split<T, ROWS, W, 2, 0, NTL, kSpanLocal>),
+                       dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v2, b.v,
+                       ng, 0u, b.n, c0, q0, q1, (T)0, (uint32_t)k, 1u << 30, 0u,
+                       b.st);
+  });
+  float rem = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round_split<T, ROWS, W, 2, 0, NT, kSpanRemote>),
+                       dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v2, b.v,
+                       ng, 0u, b.n, c0, q0, q1, (T)0, (uint32_t)k, 1u << 30, 0u,
+                       b.st);
+  });
+  float both = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round_split<T, ROWS, W, 2, 0, NTL, kSpanLocal>),
+                       dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v2, b.v,
+                       ng, 0u, b.n, c0, q0, q1, (T)0, (uint32_t)k, 1u << 30, 0u,
+                       b.st);
+    hipLaunchKernelGGL((k_round_split<T, ROWS, W, 2, 0, NT, kSpanRemote>),
+                       dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v2, b.v,
+                       ng, 0u, b.n, c0, q0, q1, (T)0, (uint32_t)k, 1u << 30, 0u,
+                       b.st);
+  });
+  std::printf("  split rows=%d nt=%d ntl=%d grid=%4u local=[%u,%u)  k_round %8.4f  "
+              "local %8.4f  remote %8.4f  local+remote %8.4f ms\n",
+              ROWS, NT, NTL, grid, c0, c0 + b.nr, one, loc, rem, both);
+}
+
 template <typename T, int ROWS, bool NT, bool ALT>
 static void
 mfree_seq(const Bufs<T>& b, unsigned cap)
@@ -171,6 +214,23 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_SPLIT")) { // split-round cost only
+    const unsigned c0 = b.nr < b.n ? b.n / 2 - b.nr / 2 : 0;
+    const unsigned c0a = c0 - c0 % 64;
+    split_seq<T, 2, kCached>(b, 256, c0a);
+    split_seq<T, 4, kCached>(b, 256, c0a);
+    split_seq<T, 2, kCached, kNtBoth>(b, 256, c0a);
+    split_seq<T, 4, kCached, kNtBoth>(b, 256, c0a);
+    split_seq<T, 2, kCached, kNtLoads>(b, 256, c0a);
+    split_seq<T, 2, kCached, kNtStores>(b, 256, c0a);
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   // k_round cache policy: nt = 0 cached, 1 non-temporal loads, 2
   // non-temporal stores, 3 both; U = chunks in flight per lane per row
   const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
