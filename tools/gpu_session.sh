@@ -45,6 +45,9 @@ for s in $STEPS; do
       make -s -C tools bench_hilbert
       step bench_hilbert_f32 300 ./tools/bench_hilbert f32
       step bench_hilbert_f64 300 ./tools/bench_hilbert f64 ;;
+    kernels)
+      make -s -C tools bench_kernels
+      step bench_kernels 300 ./tools/bench_kernels ;;
     multi) # the N > 1 bench path rehearsed on one GPU (gloo exchange)
       step bench_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu
       step bench_p4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 20 --warmup 3 --backend gloo --one-gpu ;;
