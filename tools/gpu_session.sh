@@ -48,6 +48,9 @@ for s in $STEPS; do
     kernels)
       make -s -C tools bench_kernels
       step bench_kernels 300 ./tools/bench_kernels ;;
+    h2d)
+      make -s -C tools h2d_probe
+      step h2d_probe 300 ./tools/h2d_probe 64 256 512 2048 ;;
     multi) # the N > 1 bench path rehearsed on one GPU (gloo exchange)
       step bench_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu
       step bench_p4 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29513 bench.py --gpus 4 --steps 20 --warmup 3 --backend gloo --one-gpu ;;
