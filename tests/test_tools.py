@@ -1,0 +1,70 @@
+"""CPU: the measurement tools' arithmetic (tools/pmc_traffic.py,
+tools/sweep_table.py) on synthetic rocprofv3 / sweep output."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOOLS = os.path.join(REPO, "tools")
+
+KR = "void st::dev::k_round<double, 4, 2, 2, 0, 0, 256, true>(double*, double const*)"
+KR32 = "void st::dev::k_round<float, 4, 4, 2, 0, 0, 256, true>(float*, float const*)"
+KM = "void st::dev::k_mfree<double, 4, 2, 2, true, 256, true>(double const*)"
+
+
+def _write(path, fields, rows):
+    with open(path, "w", newline="") as f:
+        w = csv.DictWriter(f, fieldnames=fields)
+        w.writeheader()
+        w.writerows(rows)
+
+
+def test_pmc_traffic_corrections(tmp_path):
+    n = 1024
+    algo_round = 2.0 * n * n * 8
+    # FETCH_SIZE counts half of the wide streaming reads on gfx950 (KiB)
+    fetch_kib = algo_round / 2 / 2 / 1024
+    write_kib = algo_round / 2 / 1024
+    pmc = [{"Kernel_Name": KR, "Counter_Value": fetch_kib}] * 4 + [
+        {"Kernel_Name": KR, "Counter_Value": 1.0},          # a gated no-op launch: dropped
+        {"Kernel_Name": KR32, "Counter_Value": 123.0},      # other dtype: filtered
+        {"Kernel_Name": KM, "Counter_Value": n * n * 8 / 2 / 1024}]
+    wr = [{"Kernel_Name": KR, "Counter_Value": write_kib}] * 4 + [
+        {"Kernel_Name": KR, "Counter_Value": 0.0},
+        {"Kernel_Name": KR32, "Counter_Value": 1.0},
+        {"Kernel_Name": KM, "Counter_Value": 0.0}]
+    trace = [{"Kernel_Name": KR, "Start_Timestamp": 0, "End_Timestamp": 100000}] * 4
+    _write(tmp_path / "f.csv", ["Kernel_Name", "Counter_Value"], pmc)
+    _write(tmp_path / "w.csv", ["Kernel_Name", "Counter_Value"], wr)
+    _write(tmp_path / "t.csv", ["Kernel_Name", "Start_Timestamp", "End_Timestamp"], trace)
+    out = tmp_path / "o.json"
+    subprocess.run([sys.executable, os.path.join(TOOLS, "pmc_traffic.py"), "--workload", "x",
+                    "--n", str(n), "--fetch", str(tmp_path / "f.csv"),
+                    "--write", str(tmp_path / "w.csv"), "--trace", str(tmp_path / "t.csv"),
+                    "--out", str(out)], check=True, capture_output=True)
+    d = json.load(open(out))
+    e = {x["kernel"]: x for x in d["entries"]}
+    assert set(e) == {"k_round", "k_mfree"}
+    assert abs(e["k_round"]["traffic_over_algorithmic"] - 1.0) < 1e-12
+    assert e["k_round"]["launches_used"] == 4
+    assert abs(e["k_round"]["trace_ms_avg"] - 0.1) < 1e-12
+    assert abs(e["k_mfree"]["traffic_over_algorithmic"] - 1.0) < 1e-12
+    assert d["fused_bytes_per_launch"] == e["k_round"]["hbm_bytes_per_launch"]
+
+
+def test_sweep_table(tmp_path):
+    log = tmp_path / "s.log"
+    log.write_text(
+        "n=2048 f64  matrix 0.031 GiB\n"
+        "  k_round rows=2 nt=0 alt=1 grid= 256    0.0100 ms   1.0 GB/s\n"
+        "  k_round rows=4 nt=0 alt=1 grid= 256    0.0200 ms   1.0 GB/s\n"
+        "n=1024x4096 f32  block 0.016 GiB\n"
+        "  k_round rows=2 nt=0 alt=1 grid= 256    0.0050 ms   1.0 GB/s\n"
+        "  k_mfree rows=4 nt=1 alt=1 grid= 512    0.0040 ms   1.0 GB/s\n")
+    out = subprocess.run([sys.executable, os.path.join(TOOLS, "sweep_table.py"), str(log)],
+                         check=True, capture_output=True, text=True).stdout
+    assert "1024x4096 32" in out and "2048 64" in out
+    row = [ln for ln in out.splitlines() if ln.startswith("(4, 0, 1, 256)")][0]
+    assert "2.000" in row
