@@ -107,6 +107,22 @@ k_stream_buf(d2* a, size_t n2, double f)
   }
 }
 
+// "flat" dispatch (babelstream style): one short-lived workgroup per
+// BLK*U 16-byte elements, no grid stride; MODE 0 in place, 1 copy
+template <int BLK, int U, int POL, int MODE>
+__global__ __launch_bounds__(BLK) void
+k_flat(d2* a, d2* b, double f)
+{
+  const size_t base = (size_t)blockIdx.x * BLK * U + threadIdx.x;
+  d2 x[U];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    x[u] = ld<POL>(a + base + u * BLK);
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    st<POL>((MODE == 0 ? a : b) + base + u * BLK, x[u] * f);
+}
+
 struct Bench
 {
   d2 *a, *b;
@@ -139,6 +155,31 @@ struct Bench
                 MODE == 0 ? "inpl" : (MODE == 1 ? "copy" : "read"), BLK, U, POL,
                 CHUNK ? "chunk" : "stride", grid, t[t.size() / 2],
                 bytes / (t[t.size() / 2] * 1e-3) / 1e9);
+  }
+  template <int BLK, int U, int POL, int MODE>
+  void runflat()
+  {
+    const unsigned grid = (unsigned)(n2 / ((size_t)BLK * U));
+    auto f = [&] {
+      hipLaunchKernelGGL((k_flat<BLK, U, POL, MODE>), dim3(grid), dim3(BLK), 0,
+                         0, a, b, 1.0);
+    };
+    f();
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < reps; r++) {
+      HIPCHECK(hipEventRecord(e0));
+      f();
+      HIPCHECK(hipEventRecord(e1));
+      HIPCHECK(hipEventSynchronize(e1));
+      float ms;
+      HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+      t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    std::printf("flat   %-4s blk=%4d u=%d pol=%d grid=%9u  %8.4f ms  %7.1f GB/s\n",
+                MODE == 0 ? "inpl" : "copy", BLK, U, POL, grid, t[t.size() / 2],
+                2.0 * n2 * 16 / (t[t.size() / 2] * 1e-3) / 1e9);
   }
   template <int BLK, int U, int LA, int SA>
   void runbuf(unsigned grid)
@@ -197,6 +238,20 @@ main(int argc, char** argv)
   HIPCHECK(hipEventCreate(&B.e0));
   HIPCHECK(hipEventCreate(&B.e1));
   std::printf("buffer %zu MiB, reps %d\n", mib, B.reps);
+  if (std::getenv("STREAM_FLAT")) { // babelstream-style flat dispatch only
+    B.runflat<256, 1, 0, 0>();
+    B.runflat<256, 1, 1, 0>();
+    B.runflat<256, 2, 1, 0>();
+    B.runflat<256, 4, 1, 0>();
+    B.runflat<256, 4, 0, 0>();
+    B.runflat<1024, 1, 1, 0>();
+    B.runflat<256, 1, 0, 1>();
+    B.runflat<256, 1, 1, 1>();
+    B.runflat<256, 4, 1, 1>();
+    B.grids<256, 4, 1, 0>();
+    B.grids<256, 4, 1, 1>();
+    return 0;
+  }
   B.grids<256, 4, 1, 0>();
   B.grids<256, 2, 1, 0>();
   B.bufgrids<0, 0>();
