@@ -60,8 +60,11 @@ class st_state(ctypes.Structure):
                 ("lambda_", ctypes.c_double),
                 ("max", ctypes.c_double),
                 ("end", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32),
-                ("pad", ctypes.c_uint64 * 3)]
+                ("arrivals", ctypes.c_uint32),
+                ("max_bits", ctypes.c_uint64),
+                ("fail", ctypes.c_uint32),
+                ("pad0", ctypes.c_uint32),
+                ("pad", ctypes.c_uint64 * 1)]
 
 
 assert ctypes.sizeof(st_state) == 64

@@ -560,6 +560,202 @@ k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 }
 
 // ---------------------------------------------------------------------------
+// flat round, for matrices that outgrow the memory-side cache
+//
+// tools/stream_bench.hip: an in-place stream moves 6.47 TB/s at 8 GiB when
+// every workgroup takes one 4 KB piece and exits (millions of short
+// workgroups: the chip sweeps a compact address window), against 5.62 TB/s
+// for one long stream per CU (profiles/r01_stream_flat_8GiB.log).  The
+// round then takes three launches, all gated like k_round (round k is a
+// no-op once a round j < k stopped):
+//   k_stats  m_k, stop_k, lambda and the state of round k from the FULL s_k:
+//            a grid-stride sweep, max and the failed-pair flag combined with
+//            order-independent atomics in st_state's scratch words, the last
+//            workgroup to arrive publishes and clears them          O(N)
+//   k_flat   one workgroup per (row, piece of BLK*W columns): v[r] *= s_k[r]
+//            / m_k (piece 0), A <- D^-1 A D on the piece (the element update
+//            of k_round, bit for bit), the piece's sum -> part[r][p]  2*N^2*b
+//   k_parts  s_{k+1}[r] = the pieces of row r summed in a fixed order (one
+//            wave per row)                                  N * N/(BLK*W) * b
+// The row sums are deterministic and independent of the row partition, but
+// not bitwise k_round's (pieces are summed apart).
+// ---------------------------------------------------------------------------
+template <typename T, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_stats(const T* __restrict__ s, uint32_t n, T eps, uint32_t k,
+        uint32_t max_itr, uint32_t semantics, st_state* state)
+{
+  {
+    const uint32_t e =
+      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0 && e <= k)
+      return;
+  }
+  __shared__ T mx_sh[BLK / 64];
+  const bool cyclic = semantics == ST_SEM_SYCL;
+  T mx = (T)0; // find_max starts from 0 (cpp:185): negatives and NaN never win
+  int fail = 0;
+  for (uint32_t i = blockIdx.x * BLK + threadIdx.x; i < n;
+       i += gridDim.x * BLK) {
+    const T x = s[i];
+    mx = x > mx ? x : mx;
+    if (i + 1 < n || cyclic) {
+      const T d = x - s[i + 1 < n ? i + 1 : 0];
+      fail |= (d < (T)0 ? -d : d) < eps ? 0 : 1; // cpp:419-421; NaN fails
+    }
+  }
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0)
+    mx_sh[threadIdx.x >> 6] = mx;
+  fail = __syncthreads_or(fail);
+  if (threadIdx.x == 0) {
+    T m = mx_sh[0];
+#pragma unroll
+    for (int w = 1; w < BLK / 64; w++)
+      m = mx_sh[w] > m ? mx_sh[w] : m;
+    // m >= 0 and not NaN: its bit pattern orders like its value
+    const uint64_t bits = sizeof(T) == 8
+                            ? (uint64_t)__double_as_longlong((double)m)
+                            : (uint64_t)__float_as_uint((float)m);
+    __hip_atomic_fetch_max(&state->max_bits, bits, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    if (fail)
+      __hip_atomic_fetch_or(&state->fail, 1u, __ATOMIC_RELAXED,
+                            __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t done_before = __hip_atomic_fetch_add(
+      &state->arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done_before == gridDim.x - 1) { // last arriver publishes round k
+      const uint64_t mb = __hip_atomic_load(&state->max_bits, __ATOMIC_ACQUIRE,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t f = __hip_atomic_load(&state->fail, __ATOMIC_ACQUIRE,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+      const T mk = sizeof(T) == 8 ? (T)__longlong_as_double((long long)mb)
+                                  : (T)__uint_as_float((uint32_t)mb);
+      const bool stop = f == 0;
+      state->lambda = (double)s[0]; // cpp:60-65
+      state->max = (double)mk;
+      state->stop = stop ? 1u : 0u;
+      state->round = k;
+      if (stop) {
+        state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
+        state->end = k + 1;
+        state->done = 1u;
+      } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
+        state->iters = max_itr;
+        state->end = k + 1;
+        state->done = 1u;
+      }
+      state->max_bits = 0; // scratch back to zero for the next round
+      state->fail = 0u;
+      state->arrivals = 0u;
+    }
+  }
+}
+
+template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
+          int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
+       T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
+       uint32_t row0, uint32_t k, const st_state* state)
+{
+  // R rows of one column piece per workgroup (the piece's column scales are
+  // loaded once for the R rows); PW: one partial per wave instead of a
+  // workgroup combine (no barrier before the workgroup retires)
+  {
+    const uint32_t e =
+      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0 && e <= k)
+      return;
+  }
+  using V = typename vec<T, W>::type;
+  constexpr int NW = BLK / 64;
+  __shared__ T red[NW][R];
+  const uint32_t rg = blockIdx.x / ppr;
+  const uint32_t p = blockIdx.x - rg * ppr;
+  const uint32_t c = (p * BLK + threadIdx.x) * W;
+  const uint32_t r0 = rg * R;
+  T acc[R];
+  V x[R];
+  T sr[R];
+  const bool in = c < ncols; // ncols % W == 0 on the vector path (host-checked)
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    acc[j] = (T)0;
+    if (in && r0 + j < nrows)
+      x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
+    sr[j] = r0 + j < nrows ? s_cur[row0 + r0 + j] : (T)1;
+  }
+  if (in) {
+    const V sc = *reinterpret_cast<const V*>(s_cur + c);
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      if (r0 + j < nrows) {
+        const T inv = (T)1 / sr[j];
+        V y;
+        if constexpr (ORDER == 0)
+          y = x[j] * (inv * sc); // cpp:324-325
+        else
+          y = (inv * x[j]) * sc; // main.py:13-16
+        st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c), y);
+        acc[j] = hsum<T, W>(y);
+      }
+    }
+  }
+  if (p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
+    // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats
+    const uint32_t r = row0 + r0 + threadIdx.x;
+    const T m = (T)state->max;
+    v[r] = v[r] * (s_cur[r] / m);
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    const T t = wave_sum(acc[j]);
+    if constexpr (PW) {
+      if (lane == 0 && r0 + j < nrows)
+        part[((size_t)(r0 + j) * ppr + p) * NW + wave] = t;
+    } else if (lane == 0) {
+      red[wave][j] = t;
+    }
+  }
+  if constexpr (!PW) {
+    __syncthreads();
+    if (threadIdx.x < R && r0 + threadIdx.x < nrows) {
+      T t = red[0][threadIdx.x];
+#pragma unroll
+      for (int w = 1; w < NW; w++)
+        t += red[w][threadIdx.x];
+      part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+    }
+  }
+}
+
+template <typename T, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
+        uint32_t ppr /* partials per row */, uint32_t k, const st_state* state)
+{
+  {
+    const uint32_t e =
+      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (e != 0 && e <= k)
+      return;
+  }
+  const uint32_t r = (blockIdx.x * BLK + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (r >= nrows)
+    return; // whole waves leave together
+  const T* row = part + (size_t)r * ppr;
+  T acc = (T)0;
+  for (uint32_t p = lane; p < ppr; p += 64)
+    acc += row[p];
+  acc = wave_sum(acc);
+  if (lane == 0)
+    s_next[r] = acc;
+}
+
+// ---------------------------------------------------------------------------
 // matrix-free round: the same iteration without ever
 // writing the matrix.  With v the eigenvector accumulator, the transformed
 // matrix of round k is A_k = X^-1 A_0 X for X = diag(x), x ∝ Π_{j<k} s_j,

@@ -186,8 +186,13 @@ typedef struct st_state
   double lambda;   /* s[0] of the last evaluated round                    */
   double max;      /* max row sum of the last evaluated round             */
   uint32_t end;    /* st_round_*: 1 + the round that stopped, 0 = running */
-  uint32_t reserved;
-  uint64_t pad[3];
+  /* scratch of the flat round's stats launch (st_round_flat_*); zero
+   * between launches, as st_state_reset leaves it */
+  uint32_t arrivals; /* workgroups done                                   */
+  uint64_t max_bits; /* running max (bit pattern of a value >= 0)         */
+  uint32_t fail;     /* some pair |s_i - s_{i+1}| >= eps (or NaN)          */
+  uint32_t pad0;
+  uint64_t pad[1];
 } st_state;
 
 /* zero a state (hipMemsetAsync) */

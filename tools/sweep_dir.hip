@@ -151,6 +151,62 @@ split_seq(const Bufs<T>& b, unsigned cap, unsigned c0)
               ROWS, NT, NTL, grid, c0, c0 + b.nr, one, loc, rem, both);
 }
 
+// the flat round (k_stats + k_flat + k_parts) against one k_round launch
+template <typename T, int NTF, int R, bool PW>
+static void
+flat_seq(const Bufs<T>& b, T* part)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
+  const unsigned nparts = ppr * (PW ? 4 : 1);
+  const unsigned sgrid = (b.n + 255) / 256 < 256 ? (b.n + 255) / 256 : 256;
+  const unsigned grid = (b.nr + R - 1) / R * ppr;
+  float flat = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_stats<T>), dim3(sgrid), dim3(256), 0, 0, b.s, b.n,
+                       (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+    hipLaunchKernelGGL((k_flat<T, W, 0, NTF != 0, R, PW>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr, b.n, ppr, 0u,
+                       (uint32_t)k, b.st);
+    hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
+                       part, b.sn, b.nr, nparts, (uint32_t)k, b.st);
+  });
+  float only = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_flat<T, W, 0, NTF != 0, R, PW>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr, b.n, ppr, 0u,
+                       (uint32_t)k, b.st);
+  });
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
+  std::printf("  flat nt=%d r=%d pw=%d  round (3 launches) %8.4f ms %7.1f GB/s | "
+              "k_flat alone %8.4f ms %7.1f GB/s\n",
+              NTF, R, (int)PW, flat, bytes / (flat * 1e-3) / 1e9, only,
+              bytes / (only * 1e-3) / 1e9);
+}
+
+template <typename T>
+static void
+round_ref(const Bufs<T>& b, int rows_round, unsigned cap_round)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ng = b.nr / rows_round;
+  const unsigned grid = cap_round < ng ? cap_round : ng;
+  float one;
+  if (rows_round == 2)
+    one = time_seq([&](int k) {
+      hipLaunchKernelGGL((k_round<T, 2, W, 2, 0, kNtBoth, 256, true>),
+                         dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng,
+                         0u, b.n, 0u, (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+    });
+  else
+    one = time_seq([&](int k) {
+      hipLaunchKernelGGL((k_round<T, 4, W, 2, 0, kCached, 256, true>),
+                         dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng,
+                         0u, b.n, 0u, (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+    });
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
+  std::printf("  k_round rows=%d  %8.4f ms %7.1f GB/s\n", rows_round, one,
+              bytes / (one * 1e-3) / 1e9);
+}
+
 template <typename T, int ROWS, bool NT, bool ALT>
 static void
 mfree_seq(const Bufs<T>& b, unsigned cap)
@@ -214,6 +270,27 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_FLAT")) { // the flat round vs k_round
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 255) / 256;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
+    round_ref<T>(b, big ? 2 : 4, 256);
+    flat_seq<T, 1, 1, false>(b, part);
+    flat_seq<T, 1, 1, true>(b, part);
+    flat_seq<T, 1, 2, false>(b, part);
+    flat_seq<T, 1, 2, true>(b, part);
+    flat_seq<T, 1, 4, true>(b, part);
+    flat_seq<T, 0, 2, true>(b, part);
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_SPLIT")) { // split-round cost only
     const unsigned c0 = b.nr < b.n ? b.n / 2 - b.nr / 2 : 0;
     const unsigned c0a = c0 - c0 % 64;
