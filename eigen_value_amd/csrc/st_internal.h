@@ -44,6 +44,15 @@ int launch_round(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                  uint32_t ncols, uint32_t row0, T eps, uint32_t k,
                  uint32_t max_itr, uint32_t semantics, st_state* st,
                  hipStream_t stream);
+// the flat round for large blocks (k_stats + k_flat + k_parts); `part`
+// holds round_flat_scratch(nrows, ncols) elements
+template <typename T>
+int launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                      uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+                      uint32_t k, uint32_t max_itr, uint32_t semantics,
+                      st_state* st, hipStream_t stream);
+size_t round_flat_scratch(uint32_t nrows, uint32_t ncols);
+bool round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem);
 template <typename T>
 int launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
                  T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,

@@ -99,6 +99,31 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   return { 4, true, 512u };
 }
 
+// the flat round (k_stats + k_flat + k_parts) for blocks of >= 1 GiB:
+// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat.log (32768^2
+// fp64 2.73 ms vs 3.06 for k_round; 16384^2 0.72 vs 0.76; below 1 GiB the
+// cached k_round, which the MALL helps, stays ahead)
+constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
+
+inline bool
+flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return block_bytes(nrows, ncols, elem) >= ((size_t)1 << 30);
+}
+
+// partial sums per row (one per piece) and the scratch they need
+inline uint32_t
+flat_pieces(uint32_t ncols, int w)
+{
+  return (ncols + (uint32_t)(kBlock * w) - 1) / (uint32_t)(kBlock * w);
+}
+
+inline size_t
+flat_scratch_elems(uint32_t nrows, uint32_t ncols)
+{
+  return (size_t)nrows * flat_pieces(ncols, 1); // enough for any vector width
+}
+
 inline bool
 fused_nt(uint32_t nrows, uint32_t ncols, size_t elem)
 {
@@ -406,6 +431,76 @@ launch_round_split(int span, T* a, const T* s_cur, T* s_next, T* part, T* v,
   return check_launch("round_split");
 }
 
+template <typename T, int W, int ORDER>
+void
+launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                  uint32_t nrows, uint32_t ncols, uint32_t row0, uint32_t k,
+                  st_state* st, hipStream_t stream)
+{
+  const uint32_t ppr = flat_pieces(ncols, W);
+  const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
+  hipLaunchKernelGGL(
+    (dev::k_flat<T, W, ORDER, true, kFlatRows, false>), dim3(grid),
+    dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
+    st);
+  hipLaunchKernelGGL((dev::k_parts<T>), dim3((nrows + dev::kWaves - 1) / dev::kWaves),
+                     dim3(kBlock), 0, stream, part, s_next, nrows, ppr, k, st);
+}
+
+template <typename T>
+int
+launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
+                  uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+                  uint32_t k, uint32_t max_itr, uint32_t semantics,
+                  st_state* st, hipStream_t stream)
+{
+  ST_REQUIRE(a && s_cur && s_next && part && v && st,
+             "round_flat: null pointer");
+  ST_REQUIRE(ncols > 0 && nrows > 0, "round_flat: empty block");
+  ST_REQUIRE(row0 + (uint64_t)nrows <= ncols,
+             "round_flat: rows [%u, %u) outside the %u-long row-sum vector",
+             row0, row0 + nrows, ncols);
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "round_flat: bad semantics %u",
+             semantics);
+  ST_REQUIRE(max_itr > 0, "round_flat: max_itr must be > 0");
+  ST_REQUIRE((uint64_t)((nrows + kFlatRows - 1) / kFlatRows) *
+                 flat_pieces(ncols, 1) <
+               (1ull << 31),
+             "round_flat: %u x %u is too large for one launch", nrows, ncols);
+  // m_k, stop_k, lambda and the state of round k from the full s_k
+  const uint32_t sgrid = (ncols + kBlock - 1) / kBlock < 256u
+                           ? (ncols + kBlock - 1) / kBlock
+                           : 256u;
+  hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
+                     s_cur, ncols, eps, k, max_itr, semantics, st);
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && aligned16(a) && aligned16(s_cur);
+  const bool order1 = semantics == ST_SEM_MAINPY;
+  if (vec_ok)
+    order1 ? launch_flat_parts<T, W, 1>(a, s_cur, s_next, part, v, nrows,
+                                        ncols, row0, k, st, stream)
+           : launch_flat_parts<T, W, 0>(a, s_cur, s_next, part, v, nrows,
+                                        ncols, row0, k, st, stream);
+  else
+    order1 ? launch_flat_parts<T, 1, 1>(a, s_cur, s_next, part, v, nrows,
+                                        ncols, row0, k, st, stream)
+           : launch_flat_parts<T, 1, 0>(a, s_cur, s_next, part, v, nrows,
+                                        ncols, row0, k, st, stream);
+  return check_launch("round_flat");
+}
+
+size_t
+round_flat_scratch(uint32_t nrows, uint32_t ncols)
+{
+  return flat_scratch_elems(nrows, ncols);
+}
+
+bool
+round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return flat_round_pays(nrows, ncols, elem);
+}
+
 template <typename T>
 int
 launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
@@ -517,6 +612,14 @@ template int launch_round<double>(double*, const double*, double*, double*,
                                   uint32_t, uint32_t, uint32_t, double,
                                   uint32_t, uint32_t, uint32_t, st_state*,
                                   hipStream_t);
+template int launch_round_flat<float>(float*, const float*, float*, float*,
+                                     float*, uint32_t, uint32_t, uint32_t,
+                                     float, uint32_t, uint32_t, uint32_t,
+                                     st_state*, hipStream_t);
+template int launch_round_flat<double>(double*, const double*, double*,
+                                      double*, double*, uint32_t, uint32_t,
+                                      uint32_t, double, uint32_t, uint32_t,
+                                      uint32_t, st_state*, hipStream_t);
 template int launch_mfree<float>(const float*, const float*, float*,
                                  const float*, float*, uint32_t, uint32_t,
                                  uint32_t, float, uint32_t, uint32_t, uint32_t,
@@ -604,6 +707,18 @@ st_state_reset(st_state* d_state, void* stream)
                                row0, eps, k, max_itr, semantics, d_state,      \
                                ST_STREAM(stream));                             \
   }                                                                            \
+  int st_round_flat_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,            \
+                          T* d_part, T* d_v, unsigned int nrows,               \
+                          unsigned int ncols, unsigned int row0, T eps,        \
+                          unsigned int k, unsigned int max_itr,                \
+                          unsigned int semantics, st_state* d_state,           \
+                          void* stream)                                        \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_round_flat<T>(d_mat, d_s_cur, d_s_next, d_part, d_v,     \
+                                    nrows, ncols, row0, eps, k, max_itr,       \
+                                    semantics, d_state, ST_STREAM(stream));    \
+  }                                                                            \
   int st_round_split_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,           \
                            T* d_part, T* d_v, unsigned int nrows,              \
                            unsigned int ncols, unsigned int row0,              \
@@ -641,5 +756,17 @@ st_state_reset(st_state* d_state, void* stream)
 
 ST_STEP_EXPORTS(float, f32)
 ST_STEP_EXPORTS(double, f64)
+
+uint64_t
+st_round_flat_scratch(unsigned int nrows, unsigned int ncols)
+{
+  return st::round_flat_scratch(nrows, ncols);
+}
+
+int
+st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype)
+{
+  return st::round_flat_pays(nrows, ncols, dtype == 1 ? 8 : 4) ? 1 : 0;
+}
 
 } // extern "C"

@@ -65,6 +65,7 @@ struct Shard
   T* a = nullptr;
   T* s[2] = { nullptr, nullptr };
   T* v[2] = { nullptr, nullptr };
+  T* part = nullptr; // flat-round partial sums (large blocks)
   st_state* state = nullptr;
 };
 
@@ -87,6 +88,7 @@ struct Multi
         (void)hipFree(d.s[i]);
         (void)hipFree(d.v[i]);
       }
+      (void)hipFree(d.part);
       (void)hipFree(d.state);
       if (d.stream)
         (void)hipStreamDestroy(d.stream);
@@ -167,6 +169,8 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
     for (int i = 0; i < (mfree ? 2 : 1); i++)
       ST_CHECK(hipMalloc(&d.v[i], sizeof(T) * (size_t)P * chunk));
     ST_CHECK(hipMalloc(&d.state, sizeof(st_state)));
+    if (!mfree && round_flat_pays(d.nrows, n, sizeof(T)))
+      ST_CHECK(hipMalloc(&d.part, sizeof(T) * round_flat_scratch(d.nrows, n)));
     ST_CHECK(hipMemsetAsync(d.state, 0, sizeof(st_state), d.stream));
     if (gen_kind == 0) {
       ST_CHECK(hipMemcpyAsync(d.a, mat + (size_t)d.row0 * n,
@@ -237,6 +241,10 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
                                d.v[k & 1], d.v[(k + 1) & 1], d.nrows, n,
                                d.row0, eps, k + 1, max_itr, sem, d.state,
                                d.stream);
+        else if (d.part)
+          rc = launch_round_flat<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk,
+                                    d.part, d.v[0], d.nrows, n, d.row0, eps, k,
+                                    max_itr, sem, d.state, d.stream);
         else
           rc = launch_round<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk, d.v[0],
                                d.nrows, n, d.row0, eps, k, max_itr, sem,

@@ -7,7 +7,8 @@
 //
 // Round loop (one device stream, no per-round host sync):
 //   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
-//   per round k, ONE launch (k_round, st_device.h):
+//   per round k, ONE launch (k_round, st_device.h; matrices of >= 1 GiB
+//   take the flat round, k_stats + k_flat + k_parts, instead):
 //     from s_k: max, v *= s/m, stop test, lambda = s_k[0] (every workgroup
 //     derives m_k/stop_k from its own sweep of s_k; workgroup 0 records)
 //     A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})
@@ -63,6 +64,8 @@ struct Context
   size_t mat_bytes = 0;
   void* d_vec = nullptr; // [s0 | s1 | v | v'], each vec_bytes
   size_t vec_bytes = 0;
+  void* d_part = nullptr; // flat-round partial sums (large matrices)
+  size_t part_bytes = 0;
   st_state* d_state = nullptr;
   st_state* h_state = nullptr; // pinned, 2 slots
   hipEvent_t ev_flag[2] = { nullptr, nullptr };
@@ -96,6 +99,22 @@ ensure_vectors(Context* c, size_t vec_bytes)
   }
   ST_CHECK(hipMalloc(&c->d_vec, 4 * vec_bytes));
   c->vec_bytes = vec_bytes;
+  return 0;
+}
+
+int
+ensure_part(Context* c, size_t bytes)
+{
+  if (c->d_part && c->part_bytes >= bytes)
+    return 0;
+  if (c->d_part) {
+    ST_CHECK(hipStreamSynchronize(c->stream));
+    ST_CHECK(hipFree(c->d_part));
+    c->d_part = nullptr;
+    c->part_bytes = 0;
+  }
+  ST_CHECK(hipMalloc(&c->d_part, bytes));
+  c->part_bytes = bytes;
   return 0;
 }
 
@@ -178,6 +197,11 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   T* vb[2] = { d_v, d_v2 };
   const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
   const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
+  // large matrices: the flat round (k_stats + k_flat + k_parts)
+  const bool flat = !mfree && round_flat_pays(n, n, sizeof(T));
+  if (flat && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
+    return -1;
+  T* d_part = reinterpret_cast<T*>(c->d_part);
   // timing events [rowsum_a, rowsum_b, (round_a, round_b)*], destroyed on
   // every exit path
   struct Events
@@ -231,6 +255,10 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
         rc |= launch_mfree<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], vb[k & 1],
                               vb[(k + 1) & 1], n, n, 0, eps, k + 1, o.max_itr,
                               o.semantics, c->d_state, s);
+      else if (flat)
+        rc |= launch_round_flat<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_part,
+                                   d_v, n, n, 0, eps, k, o.max_itr,
+                                   o.semantics, c->d_state, s);
       else
         rc |= launch_round<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_v, n, n, 0,
                               eps, k, o.max_itr, o.semantics, c->d_state, s);
@@ -413,6 +441,8 @@ destroy_queue(void* wq)
     (void)hipFree(c->d_mat);
   if (c->d_vec)
     (void)hipFree(c->d_vec);
+  if (c->d_part)
+    (void)hipFree(c->d_part);
   if (c->d_state)
     (void)hipFree(c->d_state);
   if (c->h_state)

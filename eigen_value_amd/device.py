@@ -156,6 +156,37 @@ def mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0: int = 0,
         row0, eps, k, max_itr, semantics, _ptr(state), _stream(mat0.device)), "mfree_round")
 
 
+def flat_round_pays(nrows: int, ncols: int, dtype) -> bool:
+    """Whether the flat round (st_round_flat) is the faster form for a block."""
+    torch = _torch()
+    return bool(_lib.load().st_round_flat_pays(nrows, ncols,
+                                               1 if dtype == torch.float64 else 0))
+
+
+def flat_scratch(nrows: int, ncols: int, dtype, device=None):
+    """Partial-sum scratch for flat_round on this block."""
+    torch = _torch()
+    n = int(_lib.load().st_round_flat_scratch(nrows, ncols))
+    return torch.empty(n, dtype=dtype, device=device or "cuda")
+
+
+def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float = 0.0,
+               k: int = 0, max_itr: int = _lib.ST_MAX_ITR,
+               semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """Round k as three launches for large blocks (st_round_flat): stats of
+    the full s_cur, the transform in short per-piece workgroups, the
+    pieces' partial sums into s_next.  Same contract as fused_round."""
+    _check_cuda(mat, s_cur, s_next, part, v, state)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    assert s_cur.numel() >= ncols and s_next.numel() >= nrows and v.numel() >= ncols
+    assert row0 + nrows <= ncols
+    assert part.numel() >= int(_lib.load().st_round_flat_scratch(nrows, ncols))
+    _lib.check(getattr(_lib.load(), f"st_round_flat_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(s_next), _ptr(part), _ptr(v), nrows, ncols, row0,
+        eps, k, max_itr, semantics, _ptr(state), _stream(mat.device)), "round_flat")
+
+
 SPAN_LOCAL = 1
 SPAN_REMOTE = 2
 

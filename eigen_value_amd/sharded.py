@@ -65,6 +65,7 @@ class HipShardOps:
         from . import device as dev
         self.torch, self.dev = torch, dev
         self.device = torch.device(device or "cuda")
+        self._part = None   # flat-round scratch, (shape key, tensor)
 
     def empty(self, shape, dtype):
         return self.torch.empty(shape, dtype=dtype, device=self.device)
@@ -95,8 +96,18 @@ class HipShardOps:
         self.dev.epilogue(s, v, state, eps, max_itr, semantics)
 
     def round(self, mat, s_cur, s_next, v, row0, eps, k, max_itr, semantics, state):
-        self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
-                       max_itr=max_itr, semantics=semantics, state=state)
+        # blocks of >= 1 GiB take the flat round (st_round_flat), the rest the
+        # one-launch k_round
+        nrows, ncols = mat.shape
+        if self.dev.flat_round_pays(nrows, ncols, mat.dtype):
+            key = (nrows, ncols, mat.dtype)
+            if self._part is None or self._part[0] != key:
+                self._part = (key, self.dev.flat_scratch(nrows, ncols, mat.dtype, self.device))
+            self.dev.flat_round(mat, s_cur, s_next, self._part[1], v, state, row0=row0,
+                                eps=eps, k=k, max_itr=max_itr, semantics=semantics)
+        else:
+            self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
+                                 max_itr=max_itr, semantics=semantics, state=state)
 
     def split_round(self, mat, s_cur, s_next, part, v, row0, col0, col1, eps, k, max_itr,
                     semantics, state, span):

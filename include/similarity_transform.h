@@ -269,6 +269,30 @@ int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                  unsigned int max_itr, unsigned int semantics,
                  st_state* d_state, void* stream);
 
+/* The same round for large blocks as three launches (k_stats, k_flat,
+ * k_parts in st_device.h): m_k / stop_k / lambda / state from the full s_k,
+ * then one short workgroup per (2 rows, 256 x 16-byte column piece) for
+ * the v update and the in-place transform (the HBM serves many short
+ * workgroups sweeping a compact address window faster than one long stream
+ * per CU), then the pieces' partial sums into s_next in a fixed order.
+ * Results as st_round_* except the row sums' summation order (deterministic
+ * and independent of the row partition).  d_part: scratch of
+ * st_round_flat_scratch(nrows, ncols) elements.  st_round_flat_pays tells
+ * whether this form is the faster one for a block (dtype 0 = f32, 1 = f64);
+ * the library's own solve loops use it for such blocks. */
+int st_round_flat_f32(float* d_mat, const float* d_s_cur, float* d_s_next,
+                      float* d_part, float* d_v, unsigned int nrows,
+                      unsigned int ncols, unsigned int row0, float eps,
+                      unsigned int k, unsigned int max_itr,
+                      unsigned int semantics, st_state* d_state, void* stream);
+int st_round_flat_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
+                      double* d_part, double* d_v, unsigned int nrows,
+                      unsigned int ncols, unsigned int row0, double eps,
+                      unsigned int k, unsigned int max_itr,
+                      unsigned int semantics, st_state* d_state, void* stream);
+uint64_t st_round_flat_scratch(unsigned int nrows, unsigned int ncols);
+int st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype);
+
 /* Round k split in two launches for a sharded solve that overlaps the
  * all-gather of s_k with compute (eigen_value_amd/sharded.py, overlap).
  * [col0, col1) are the columns whose s_k values this rank computed itself

@@ -158,6 +158,68 @@ def test_round_kernel_vs_oracle(orc, dt, sem, nrows, ncols, row0):
     assert st["stop"] == int(orc.stop(s_full, eps=dt(1e-3), cyclic=sem == _lib.ST_SEM_SYCL))
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
+@pytest.mark.parametrize("nrows,ncols,row0", [(1, 1, 0), (3, 3, 0), (7, 257, 100), (1025, 2048, 1000),
+                                              (2049, 3000, 0), (1500, 1501, 0)])
+def test_flat_round_vs_round(orc, dt, sem, nrows, ncols, row0):
+    """st_round_flat_* (k_stats + k_flat + k_parts) against st_round_* and the
+    oracle: A_{k+1} and v bit for bit, the state identical, s_{k+1} to
+    rounding (pieces summed apart)."""
+    if row0 + nrows > ncols:
+        pytest.skip("row block must lie inside the s vector")
+    a = orc.random_matrix(ncols, 3, dt, nrows=nrows)
+    s_full = np.ascontiguousarray((orc.random_matrix(ncols, 9, dt, nrows=1)[0]
+                                   + dt(0.5)).astype(dt))
+    v0 = orc.random_matrix(ncols, 5, dt, nrows=1)[0]
+    outs = []
+    for flat in (False, True):
+        ta, ts, tv = (torch.from_numpy(x).to(DEV) for x in (a, s_full, v0))
+        s_next = torch.empty(nrows, dtype=TD[dt], device=DEV)
+        state = dev.new_state(DEV)
+        if flat:
+            part = dev.flat_scratch(nrows, ncols, TD[dt], DEV)
+            dev.flat_round(ta, ts, s_next, part, tv, state, row0=row0, eps=1e-3, k=2,
+                           semantics=sem)
+        else:
+            dev.fused_round(ta, ts, s_next, tv, state, row0=row0, eps=1e-3, k=2, semantics=sem)
+        outs.append((to_np(ta), to_np(s_next), to_np(tv), dev.read_state(state)))
+    (a0, s0, v0_, st0), (a1, s1, v1, st1) = outs
+    ref = orc.compute_next(a, s_full, row0=row0, order=0 if sem == _lib.ST_SEM_SYCL else 1)
+    assert np.array_equal(a1, ref) and np.array_equal(a1, a0)
+    assert np.array_equal(v1, v0_) and st1 == st0
+    tol = 1e-13 if dt == np.float64 else 2e-6
+    ref_s = orc.rowsum(ref)
+    assert np.max(np.abs(s1 - ref_s) / np.abs(ref_s)) <= tol
+
+
+def test_flat_round_stats_and_gating(orc):
+    """k_stats: max ignores negatives and NaN (find_max starts at 0), a NaN
+    pair fails the stop test, the stopping round sets end = k+1 and later
+    flat rounds are no-ops; the scratch words are left zeroed."""
+    n = 700
+    a = torch.from_numpy(orc.random_matrix(n, 1)).to(DEV)
+    s = torch.full((n,), 4.0, dtype=torch.float64, device=DEV)     # constant: stops
+    s_next = torch.empty_like(s)
+    v = torch.ones_like(s)
+    part = dev.flat_scratch(n, n, torch.float64, DEV)
+    state = dev.new_state(DEV)
+    dev.flat_round(a, s, s_next, part, v, state, k=0)
+    st = dev.read_state(state)
+    assert st["stop"] == 1 and st["done"] == 1 and st["end"] == 1 and st["max"] == 4.0
+    keep = a.clone()
+    dev.flat_round(a, s * 2.0, s_next, part, v, state, k=1)       # gated
+    assert torch.equal(a, keep)
+    raw = _lib.st_state.from_buffer_copy(state.cpu().numpy().tobytes())
+    assert raw.arrivals == 0 and raw.max_bits == 0 and raw.fail == 0
+    s2 = torch.full((n,), 2.0, dtype=torch.float64, device=DEV)
+    s2[5], s2[6] = -7.0, float("nan")
+    state2 = dev.new_state(DEV)
+    dev.flat_round(a, s2, s_next, part, v, state2, k=0, max_itr=10)
+    st2 = dev.read_state(state2)
+    assert st2["max"] == 2.0 and st2["stop"] == 0 and st2["done"] == 0
+
+
 def test_round_stop_and_gating(orc):
     n = 600
     a = torch.from_numpy(orc.random_matrix(n, 1)).to(DEV)
@@ -229,9 +291,11 @@ def test_sharded_overlap_single_gpu_bitwise(solver):
     assert l0 == l1 and i0 == i1 and r0 == r1 and torch.equal(v0, v1)
 
 
-def test_sharded_single_gpu_matches_device_solver(solver):
+@pytest.mark.parametrize("n", [3000, 16384])
+def test_sharded_single_gpu_matches_device_solver(solver, n):
+    """P = 1 sharded driver == the library's solve loop, bit for bit, for the
+    one-launch round (3000²) and the flat round (16384², 2 GiB)."""
     from eigen_value_amd.sharded import ShardedSimilarityTransform
-    n = 3000
     sh = ShardedSimilarityTransform(n, torch.float64)
     sh.load("hilbert")
     lam, v, iters, rounds = sh.solve(eps=1e-3)

@@ -56,8 +56,8 @@ def main():
     a = ap.parse_args()
     fetch, write = load_pmc(a.fetch), load_pmc(a.write)
     trace = load_trace(a.trace) if a.trace else {}
-    algo = {"k_round": 2.0 * a.n * a.n * a.elem, "k_mfree": 1.0 * a.n * a.n * a.elem,
-            "k_fused": 1.0 * a.n * a.n * a.elem}
+    algo = {"k_round": 2.0 * a.n * a.n * a.elem, "k_flat": 2.0 * a.n * a.n * a.elem,
+            "k_mfree": 1.0 * a.n * a.n * a.elem, "k_fused": 1.0 * a.n * a.n * a.elem}
     entries = []
     for key in sorted(fetch):
         kname, full = key
@@ -82,7 +82,7 @@ def main():
             e["trace_launches"] = len(d)
             e["achieved_gbs_from_trace"] = algo[kname] / (e["trace_ms_avg"] * 1e-3) / 1e9
         entries.append(e)
-    fused = [e for e in entries if e["kernel"] == "k_round"]
+    fused = [e for e in entries if e["kernel"] in ("k_round", "k_flat")]
     doc = {"workload": a.workload, "n": a.n, "entries": entries,
            "fused_bytes_per_launch": fused[0]["hbm_bytes_per_launch"] if fused else None}
     json.dump(doc, open(a.out, "w"), indent=1)
