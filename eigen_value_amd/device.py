@@ -170,7 +170,7 @@ def flat_scratch(nrows: int, ncols: int, dtype, device=None):
     return torch.empty(n, dtype=dtype, device=device or "cuda")
 
 
-def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float = 0.0,
+def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float = 1e-3,
                k: int = 0, max_itr: int = _lib.ST_MAX_ITR,
                semantics: int = _lib.ST_SEM_SYCL) -> None:
     """Round k as three launches for large blocks (st_round_flat): stats of
@@ -192,7 +192,7 @@ SPAN_REMOTE = 2
 
 
 def split_round(mat, s_cur, s_next, part, v, state, *, span: int, row0: int = 0,
-                col0: int = 0, col1: Optional[int] = None, eps: float = 0.0, k: int = 0,
+                col0: int = 0, col1: Optional[int] = None, eps: float = 1e-3, k: int = 0,
                 max_itr: int = _lib.ST_MAX_ITR, semantics: int = _lib.ST_SEM_SYCL) -> None:
     """Half of a round (st_round_split): ``span=SPAN_LOCAL`` transforms the
     columns [col0, col1) and writes their row sums to ``part``;
