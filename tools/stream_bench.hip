@@ -123,6 +123,25 @@ k_flat(d2* a, d2* b, double f)
     st<POL>((MODE == 0 ? a : b) + base + u * BLK, x[u] * f);
 }
 
+// flat read-only: one short workgroup per BLK*U 16-byte elements, a
+// per-workgroup sum written out (like a row-piece partial)
+template <int BLK, int U, int POL>
+__global__ __launch_bounds__(BLK) void
+k_flat_read(const d2* a, double* part)
+{
+  const size_t base = (size_t)blockIdx.x * BLK * U + threadIdx.x;
+  double acc = 0;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const d2 x = ld<POL>(a + base + u * BLK);
+    acc += x[0] + x[1];
+  }
+  for (int off = 32; off > 0; off >>= 1)
+    acc += __shfl_down(acc, off, 64);
+  if ((threadIdx.x & 63) == 0)
+    part[(size_t)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6)] = acc;
+}
+
 struct Bench
 {
   d2 *a, *b;
@@ -181,6 +200,32 @@ struct Bench
                 MODE == 0 ? "inpl" : "copy", BLK, U, POL, grid, t[t.size() / 2],
                 2.0 * n2 * 16 / (t[t.size() / 2] * 1e-3) / 1e9);
   }
+  double* part = nullptr;
+  template <int BLK, int U, int POL>
+  void runflatread()
+  {
+    const unsigned grid = (unsigned)(n2 / ((size_t)BLK * U));
+    auto f = [&] {
+      hipLaunchKernelGGL((k_flat_read<BLK, U, POL>), dim3(grid), dim3(BLK), 0,
+                         0, a, part);
+    };
+    f();
+    HIPCHECK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < reps; r++) {
+      HIPCHECK(hipEventRecord(e0));
+      f();
+      HIPCHECK(hipEventRecord(e1));
+      HIPCHECK(hipEventSynchronize(e1));
+      float ms;
+      HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+      t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    std::printf("flat   read blk=%4d u=%d pol=%d grid=%9u  %8.4f ms  %7.1f GB/s\n",
+                BLK, U, POL, grid, t[t.size() / 2],
+                1.0 * n2 * 16 / (t[t.size() / 2] * 1e-3) / 1e9);
+  }
   template <int BLK, int U, int LA, int SA>
   void runbuf(unsigned grid)
   {
@@ -238,6 +283,20 @@ main(int argc, char** argv)
   HIPCHECK(hipEventCreate(&B.e0));
   HIPCHECK(hipEventCreate(&B.e1));
   std::printf("buffer %zu MiB, reps %d\n", mib, B.reps);
+  if (std::getenv("STREAM_FLAT_READ")) { // flat read-only variants
+    HIPCHECK(hipMalloc(&B.part, B.n2 / 64 * 8 + 64));
+    B.runflatread<256, 1, 1>();
+    B.runflatread<256, 2, 1>();
+    B.runflatread<256, 4, 1>();
+    B.runflatread<256, 1, 0>();
+    B.runflatread<256, 2, 0>();
+    B.runflatread<256, 4, 0>();
+    B.runflatread<512, 2, 1>();
+    B.runflatread<1024, 1, 1>();
+    B.grids<256, 4, 1, 2>();
+    B.grids<256, 2, 0, 2>();
+    return 0;
+  }
   if (std::getenv("STREAM_FLAT")) { // babelstream-style flat dispatch only
     B.runflat<256, 1, 0, 0>();
     B.runflat<256, 1, 1, 0>();
