@@ -580,6 +580,53 @@ k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 // The row sums are deterministic and independent of the row partition, but
 // not bitwise k_round's (pieces are summed apart).
 // ---------------------------------------------------------------------------
+// thread 0 of each of `nwg` participating workgroups: fold the workgroup's
+// max (>= 0, not NaN) and failed-pair flag into st_state's scratch words;
+// the last of them to arrive publishes round k (exactly k_round's
+// bookkeeping) and clears the scratch
+template <typename T>
+__device__ __forceinline__ void
+stats_publish(T m, int fail, uint32_t nwg, const T* __restrict__ s, uint32_t k,
+              uint32_t max_itr, uint32_t semantics, st_state* state)
+{
+  // m >= 0 and not NaN: its bit pattern orders like its value
+  const uint64_t bits = sizeof(T) == 8 ? (uint64_t)__double_as_longlong((double)m)
+                                       : (uint64_t)__float_as_uint((float)m);
+  __hip_atomic_fetch_max(&state->max_bits, bits, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  if (fail)
+    __hip_atomic_fetch_or(&state->fail, 1u, __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t done_before = __hip_atomic_fetch_add(
+    &state->arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (done_before != nwg - 1)
+    return;
+  // last arriver publishes round k
+  const uint64_t mb = __hip_atomic_load(&state->max_bits, __ATOMIC_ACQUIRE,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t f =
+    __hip_atomic_load(&state->fail, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+  const T mk = sizeof(T) == 8 ? (T)__longlong_as_double((long long)mb)
+                              : (T)__uint_as_float((uint32_t)mb);
+  const bool stop = f == 0;
+  state->lambda = (double)s[0]; // cpp:60-65
+  state->max = (double)mk;
+  state->stop = stop ? 1u : 0u;
+  state->round = k;
+  if (stop) {
+    state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
+    state->end = k + 1;
+    state->done = 1u;
+  } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
+    state->iters = max_itr;
+    state->end = k + 1;
+    state->done = 1u;
+  }
+  state->max_bits = 0; // scratch back to zero for the next round
+  state->fail = 0u;
+  state->arrivals = 0u;
+}
+
 template <typename T, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_stats(const T* __restrict__ s, uint32_t n, T eps, uint32_t k,
@@ -613,52 +660,21 @@ k_stats(const T* __restrict__ s, uint32_t n, T eps, uint32_t k,
 #pragma unroll
     for (int w = 1; w < BLK / 64; w++)
       m = mx_sh[w] > m ? mx_sh[w] : m;
-    // m >= 0 and not NaN: its bit pattern orders like its value
-    const uint64_t bits = sizeof(T) == 8
-                            ? (uint64_t)__double_as_longlong((double)m)
-                            : (uint64_t)__float_as_uint((float)m);
-    __hip_atomic_fetch_max(&state->max_bits, bits, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    if (fail)
-      __hip_atomic_fetch_or(&state->fail, 1u, __ATOMIC_RELAXED,
-                            __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t done_before = __hip_atomic_fetch_add(
-      &state->arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (done_before == gridDim.x - 1) { // last arriver publishes round k
-      const uint64_t mb = __hip_atomic_load(&state->max_bits, __ATOMIC_ACQUIRE,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t f = __hip_atomic_load(&state->fail, __ATOMIC_ACQUIRE,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-      const T mk = sizeof(T) == 8 ? (T)__longlong_as_double((long long)mb)
-                                  : (T)__uint_as_float((uint32_t)mb);
-      const bool stop = f == 0;
-      state->lambda = (double)s[0]; // cpp:60-65
-      state->max = (double)mk;
-      state->stop = stop ? 1u : 0u;
-      state->round = k;
-      if (stop) {
-        state->iters = semantics == ST_SEM_SYCL ? k : k + 1; // cpp:54 / py:47
-        state->end = k + 1;
-        state->done = 1u;
-      } else if (k + 1 >= max_itr) { // loop exhausted (cpp:39,54)
-        state->iters = max_itr;
-        state->end = k + 1;
-        state->done = 1u;
-      }
-      state->max_bits = 0; // scratch back to zero for the next round
-      state->fail = 0u;
-      state->arrivals = 0u;
-    }
+    stats_publish<T>(m, fail, gridDim.x, s, k, max_itr, semantics, state);
   }
 }
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          int BLK = kBlock>
+          bool FS = false, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
-       uint32_t row0, uint32_t k, const st_state* state)
+       uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
+       uint32_t max_itr = 0, uint32_t semantics = 0)
 {
+  // FS: the first row group's workgroups (pieces 0..ppr-1, together all of
+  // s_k) also fold m_k / stop_k into the state (stats_publish); the v update
+  // then moves to k_parts, after m_k is known
   // R rows of one column piece per workgroup (the piece's column scales are
   // loaded once for the R rows); PW: one partial per wave instead of a
   // workgroup combine (no barrier before the workgroup retires)
@@ -686,6 +702,30 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
     sr[j] = r0 + j < nrows ? s_cur[row0 + r0 + j] : (T)1;
   }
+  if constexpr (FS) {
+    if (rg == 0) { // uniform per workgroup
+      __shared__ T mx_sh[NW];
+      T mx = (T)0;
+      int ok = 1;
+      if (in) {
+        const V sc0 = *reinterpret_cast<const V*>(s_cur + c);
+        stats_at<T, W>(s_cur, sc0, c / W, ncols, semantics == ST_SEM_SYCL, eps,
+                       mx, ok);
+      }
+      int fail = ok ? 0 : 1;
+      mx = wave_max(mx);
+      if ((threadIdx.x & 63) == 0)
+        mx_sh[threadIdx.x >> 6] = mx;
+      fail = __syncthreads_or(fail);
+      if (threadIdx.x == 0) {
+        T m = mx_sh[0];
+#pragma unroll
+        for (int w = 1; w < NW; w++)
+          m = mx_sh[w] > m ? mx_sh[w] : m;
+        stats_publish<T>(m, fail, ppr, s_cur, k, max_itr, semantics, state);
+      }
+    }
+  }
   if (in) {
     const V sc = *reinterpret_cast<const V*>(s_cur + c);
 #pragma unroll
@@ -702,7 +742,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       }
     }
   }
-  if (p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
+  if (!FS && p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
     // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats
     const uint32_t r = row0 + r0 + threadIdx.x;
     const T m = (T)state->max;
@@ -734,8 +774,12 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 template <typename T, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
-        uint32_t ppr /* partials per row */, uint32_t k, const st_state* state)
+        uint32_t ppr /* partials per row */, uint32_t k, const st_state* state,
+        const T* __restrict__ s_cur = nullptr, T* __restrict__ v = nullptr,
+        uint32_t row0 = 0)
 {
+  // v != nullptr: also v[r] *= s_k[r] / m_k (cpp:260) with m_k published by
+  // k_flat's first row group
   {
     const uint32_t e =
       __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -751,8 +795,13 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   for (uint32_t p = lane; p < ppr; p += 64)
     acc += row[p];
   acc = wave_sum(acc);
-  if (lane == 0)
+  if (lane == 0) {
     s_next[r] = acc;
+    if (v != nullptr) {
+      const T m = (T)state->max;
+      v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

@@ -104,6 +104,9 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 // fp64 2.73 ms vs 3.06 for k_round; 16384^2 0.72 vs 0.76; below 1 GiB the
 // cached k_round, which the MALL helps, stays ahead)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
+// m_k / stop_k in k_flat's first row group (two launches per round) rather
+// than in a k_stats launch of their own (three)
+constexpr bool kFlatFusedStats = false;
 
 inline bool
 flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
@@ -434,17 +437,34 @@ launch_round_split(int span, T* a, const T* s_cur, T* s_next, T* part, T* v,
 template <typename T, int W, int ORDER>
 void
 launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
-                  uint32_t nrows, uint32_t ncols, uint32_t row0, uint32_t k,
+                  uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+                  uint32_t k, uint32_t max_itr, uint32_t semantics,
                   st_state* st, hipStream_t stream)
 {
   const uint32_t ppr = flat_pieces(ncols, W);
   const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
-  hipLaunchKernelGGL(
-    (dev::k_flat<T, W, ORDER, true, kFlatRows, false>), dim3(grid),
-    dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
-    st);
-  hipLaunchKernelGGL((dev::k_parts<T>), dim3((nrows + dev::kWaves - 1) / dev::kWaves),
-                     dim3(kBlock), 0, stream, part, s_next, nrows, ppr, k, st);
+  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
+  if constexpr (kFlatFusedStats) {
+    // two launches: m_k / stop_k folded into k_flat's first row group, the
+    // v update into k_parts
+    hipLaunchKernelGGL(
+      (dev::k_flat<T, W, ORDER, true, kFlatRows, false, true>), dim3(grid),
+      dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
+      st, eps, max_itr, semantics);
+    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
+                       part, s_next, nrows, ppr, k, st, s_cur, v, row0);
+  } else {
+    const uint32_t sgrid =
+      (ncols + kBlock - 1) / kBlock < 256u ? (ncols + kBlock - 1) / kBlock : 256u;
+    hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
+                       s_cur, ncols, eps, k, max_itr, semantics, st);
+    hipLaunchKernelGGL(
+      (dev::k_flat<T, W, ORDER, true, kFlatRows, false>), dim3(grid),
+      dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
+      st, eps, max_itr, semantics);
+    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
+                       part, s_next, nrows, ppr, k, st, nullptr, nullptr, 0u);
+  }
 }
 
 template <typename T>
@@ -467,25 +487,23 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
                  flat_pieces(ncols, 1) <
                (1ull << 31),
              "round_flat: %u x %u is too large for one launch", nrows, ncols);
-  // m_k, stop_k, lambda and the state of round k from the full s_k
-  const uint32_t sgrid = (ncols + kBlock - 1) / kBlock < 256u
-                           ? (ncols + kBlock - 1) / kBlock
-                           : 256u;
-  hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
-                     s_cur, ncols, eps, k, max_itr, semantics, st);
   constexpr int W = 16 / sizeof(T);
   const bool vec_ok = (ncols % W) == 0 && aligned16(a) && aligned16(s_cur);
   const bool order1 = semantics == ST_SEM_MAINPY;
   if (vec_ok)
     order1 ? launch_flat_parts<T, W, 1>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, k, st, stream)
+                                        ncols, row0, eps, k, max_itr,
+                                        semantics, st, stream)
            : launch_flat_parts<T, W, 0>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, k, st, stream);
+                                        ncols, row0, eps, k, max_itr,
+                                        semantics, st, stream);
   else
     order1 ? launch_flat_parts<T, 1, 1>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, k, st, stream)
+                                        ncols, row0, eps, k, max_itr,
+                                        semantics, st, stream)
            : launch_flat_parts<T, 1, 0>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, k, st, stream);
+                                        ncols, row0, eps, k, max_itr,
+                                        semantics, st, stream);
   return check_launch("round_flat");
 }
 

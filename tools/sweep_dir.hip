@@ -182,6 +182,27 @@ flat_seq(const Bufs<T>& b, T* part)
               bytes / (only * 1e-3) / 1e9);
 }
 
+// the two-launch flat round: stats folded into k_flat's first row group,
+// the v update into k_parts
+template <typename T, int R>
+static void
+flat2_seq(const Bufs<T>& b, T* part)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
+  const unsigned grid = (b.nr + R - 1) / R * ppr;
+  float flat = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_flat<T, W, 0, true, R, false, true>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr, b.n, ppr, 0u,
+                       (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
+    hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
+                       part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
+  });
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
+  std::printf("  flat2 r=%d  round (2 launches) %8.4f ms %7.1f GB/s\n", R, flat,
+              bytes / (flat * 1e-3) / 1e9);
+}
+
 template <typename T>
 static void
 round_ref(const Bufs<T>& b, int rows_round, unsigned cap_round)
@@ -190,7 +211,14 @@ round_ref(const Bufs<T>& b, int rows_round, unsigned cap_round)
   const unsigned ng = b.nr / rows_round;
   const unsigned grid = cap_round < ng ? cap_round : ng;
   float one;
-  if (rows_round == 2)
+  const bool big = (double)b.nr * b.n * sizeof(T) >= (double)(1u << 30);
+  if (rows_round == 2 && !big)
+    one = time_seq([&](int k) {
+      hipLaunchKernelGGL((k_round<T, 2, W, 2, 0, kCached, 256, true>),
+                         dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng,
+                         0u, b.n, 0u, (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+    });
+  else if (rows_round == 2)
     one = time_seq([&](int k) {
       hipLaunchKernelGGL((k_round<T, 2, W, 2, 0, kNtBoth, 256, true>),
                          dim3(grid), dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng,
@@ -275,13 +303,10 @@ run(unsigned nr, unsigned n)
     const unsigned ppr = (b.n + 255) / 256;
     HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
     const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
-    round_ref<T>(b, big ? 2 : 4, 256);
-    flat_seq<T, 1, 1, false>(b, part);
-    flat_seq<T, 1, 1, true>(b, part);
+    round_ref<T>(b, big ? 2 : (b.n > 12288 ? 2 : 4), big ? 256 : 256);
     flat_seq<T, 1, 2, false>(b, part);
-    flat_seq<T, 1, 2, true>(b, part);
-    flat_seq<T, 1, 4, true>(b, part);
-    flat_seq<T, 0, 2, true>(b, part);
+    flat2_seq<T, 2>(b, part);
+    flat2_seq<T, 4>(b, part);
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
     HIPCHECK(hipFree(b.s));
