@@ -106,7 +106,7 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
 // than in a k_stats launch of their own (three)
-constexpr bool kFlatFusedStats = false;
+constexpr bool kFlatFusedStats = true;
 
 inline bool
 flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
