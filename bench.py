@@ -244,7 +244,7 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic[0],
                 "kernel": ("k_round_split local + remote (overlapped exchange)" if args.overlap
-                           else "flat round: k_stats + k_flat + k_parts" if flat
+                           else "flat round: k_flat + k_parts" if flat
                            else "k_round (fused stats + scale + row-sum)"),
                 "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
@@ -325,7 +325,7 @@ def main():
         flat_ns = dev.flat_round_pays(32768, 32768, torch.float64)
         tr = load_traffic("random32768_f64", "k_flat" if flat_ns else "k_round")
         out["north_star"] = {"workload": "random32768_f64",
-                             "kernel": ("flat round: k_stats + k_flat + k_parts (round time)"
+                             "kernel": ("flat round: k_flat + k_parts (round time)"
                                         if flat_ns else "k_round"),
                              "ms_per_iteration": round(el_ns / 50 * 1e3, 4),
                              "fused_ms_avg": round(fused_ns, 4), "achieved": round(ach, 1),

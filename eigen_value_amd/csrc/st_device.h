@@ -566,19 +566,20 @@ k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 // every workgroup takes one 4 KB piece and exits (millions of short
 // workgroups: the chip sweeps a compact address window), against 5.62 TB/s
 // for one long stream per CU (profiles/r01_stream_flat_8GiB.log).  The
-// round then takes three launches, all gated like k_round (round k is a
+// round then takes two launches, both gated like k_round (round k is a
 // no-op once a round j < k stopped):
-//   k_stats  m_k, stop_k, lambda and the state of round k from the FULL s_k:
-//            a grid-stride sweep, max and the failed-pair flag combined with
-//            order-independent atomics in st_state's scratch words, the last
-//            workgroup to arrive publishes and clears them          O(N)
-//   k_flat   one workgroup per (row, piece of BLK*W columns): v[r] *= s_k[r]
-//            / m_k (piece 0), A <- D^-1 A D on the piece (the element update
-//            of k_round, bit for bit), the piece's sum -> part[r][p]  2*N^2*b
+//   k_flat   one workgroup per (2 rows, piece of BLK*W columns): A <- D^-1 A D
+//            on the piece (k_round's element update, bit for bit) and the
+//            piece's sum -> part[r][p]; the first row group's workgroups,
+//            whose pieces together cover s_k, also fold m_k and the stop
+//            test into st_state's scratch words (order-independent atomics;
+//            the last of them publishes round k, stats_publish)    2*N^2*b
 //   k_parts  s_{k+1}[r] = the pieces of row r summed in a fixed order (one
-//            wave per row)                                  N * N/(BLK*W) * b
-// The row sums are deterministic and independent of the row partition, but
-// not bitwise k_round's (pieces are summed apart).
+//            wave per row), and v[r] *= s_k[r] / m_k      N * N/(BLK*W) * b
+// (k_stats is the same stats pass as a launch of its own: the three-launch
+// form, kept for the sweep tool.)  The row sums are deterministic and
+// independent of the row partition, but not bitwise k_round's (pieces are
+// summed apart).
 // ---------------------------------------------------------------------------
 // thread 0 of each of `nwg` participating workgroups: fold the workgroup's
 // max (>= 0, not NaN) and failed-pair flag into st_state's scratch words;

@@ -44,7 +44,7 @@ int launch_round(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
                  uint32_t ncols, uint32_t row0, T eps, uint32_t k,
                  uint32_t max_itr, uint32_t semantics, st_state* st,
                  hipStream_t stream);
-// the flat round for large blocks (k_stats + k_flat + k_parts); `part`
+// the flat round for large blocks (k_flat + k_parts); `part`
 // holds round_flat_scratch(nrows, ncols) elements
 template <typename T>
 int launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,

@@ -99,7 +99,7 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   return { 4, true, 512u };
 }
 
-// the flat round (k_stats + k_flat + k_parts) for blocks of >= 1 GiB:
+// the flat round (k_flat + k_parts) for blocks of >= 1 GiB:
 // tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat.log (32768^2
 // fp64 2.73 ms vs 3.06 for k_round; 16384^2 0.72 vs 0.76; below 1 GiB the
 // cached k_round, which the MALL helps, stays ahead)

@@ -8,7 +8,7 @@
 // Round loop (one device stream, no per-round host sync):
 //   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
 //   per round k, ONE launch (k_round, st_device.h; matrices of >= 1 GiB
-//   take the flat round, k_stats + k_flat + k_parts, instead):
+//   take the flat round, k_flat + k_parts, instead):
 //     from s_k: max, v *= s/m, stop test, lambda = s_k[0] (every workgroup
 //     derives m_k/stop_k from its own sweep of s_k; workgroup 0 records)
 //     A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})
@@ -197,7 +197,7 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   T* vb[2] = { d_v, d_v2 };
   const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
   const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
-  // large matrices: the flat round (k_stats + k_flat + k_parts)
+  // large matrices: the flat round (k_flat + k_parts)
   const bool flat = !mfree && round_flat_pays(n, n, sizeof(T));
   if (flat && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
     return -1;

@@ -173,9 +173,10 @@ def flat_scratch(nrows: int, ncols: int, dtype, device=None):
 def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float = 1e-3,
                k: int = 0, max_itr: int = _lib.ST_MAX_ITR,
                semantics: int = _lib.ST_SEM_SYCL) -> None:
-    """Round k as three launches for large blocks (st_round_flat): stats of
-    the full s_cur, the transform in short per-piece workgroups, the
-    pieces' partial sums into s_next.  Same contract as fused_round."""
+    """Round k as two launches for large blocks (st_round_flat): the
+    transform in short per-piece workgroups (the first row group also takes
+    the stats of the full s_cur), then the pieces' partial sums into s_next
+    and the v update.  Same contract as fused_round."""
     _check_cuda(mat, s_cur, s_next, part, v, state)
     assert mat.is_contiguous() and mat.dim() == 2
     nrows, ncols = mat.shape

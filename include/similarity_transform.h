@@ -269,12 +269,13 @@ int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                  unsigned int max_itr, unsigned int semantics,
                  st_state* d_state, void* stream);
 
-/* The same round for large blocks as three launches (k_stats, k_flat,
- * k_parts in st_device.h): m_k / stop_k / lambda / state from the full s_k,
- * then one short workgroup per (2 rows, 256 x 16-byte column piece) for
- * the v update and the in-place transform (the HBM serves many short
- * workgroups sweeping a compact address window faster than one long stream
- * per CU), then the pieces' partial sums into s_next in a fixed order.
+/* The same round for large blocks as two launches (k_flat, k_parts in
+ * st_device.h): one short workgroup per (2 rows, 256 x 16-byte column
+ * piece) for the in-place transform (the HBM serves many short workgroups
+ * sweeping a compact address window faster than one long stream per CU),
+ * whose first row group also derives m_k / stop_k / lambda / state from the
+ * full s_k; then the pieces' partial sums into s_next in a fixed order and
+ * the eigenvector update.
  * Results as st_round_* except the row sums' summation order (deterministic
  * and independent of the row partition).  d_part: scratch of
  * st_round_flat_scratch(nrows, ncols) elements.  st_round_flat_pays tells
