@@ -100,8 +100,8 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 }
 
 // the flat round (k_flat + k_parts) for blocks of >= 1 GiB:
-// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat.log (32768^2
-// fp64 2.73 ms vs 3.06 for k_round; 16384^2 0.72 vs 0.76; below 1 GiB the
+// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat2.log (32768^2
+// fp64 2.72 ms vs 3.05 for k_round; 16384^2 0.68 vs 0.77; below 1 GiB the
 // cached k_round, which the MALL helps, stays ahead)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
