@@ -666,13 +666,15 @@ k_stats(const T* __restrict__ s, uint32_t n, T eps, uint32_t k,
 }
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          bool FS = false, int BLK = kBlock>
+          bool FS = false, bool ALT = false, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0)
 {
+  // ALT: odd rounds walk the pieces from the end of the matrix, so a round
+  // starts where the previous one finished (memory-side cache reuse)
   // FS: the first row group's workgroups (pieces 0..ppr-1, together all of
   // s_k) also fold m_k / stop_k into the state (stats_publish); the v update
   // then moves to k_parts, after m_k is known
@@ -688,8 +690,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
   __shared__ T red[NW][R];
-  const uint32_t rg = blockIdx.x / ppr;
-  const uint32_t p = blockIdx.x - rg * ppr;
+  const uint32_t b = (ALT && (k & 1u)) ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t rg = b / ppr;
+  const uint32_t p = b - rg * ppr;
   const uint32_t c = (p * BLK + threadIdx.x) * W;
   const uint32_t r0 = rg * R;
   T acc[R];

@@ -184,7 +184,7 @@ flat_seq(const Bufs<T>& b, T* part)
 
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
-template <typename T, int R>
+template <typename T, int R, bool NT = true, bool ALT = false>
 static void
 flat2_seq(const Bufs<T>& b, T* part)
 {
@@ -192,15 +192,15 @@ flat2_seq(const Bufs<T>& b, T* part)
   const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   float flat = time_seq([&](int k) {
-    hipLaunchKernelGGL((k_flat<T, W, 0, true, R, false, true>), dim3(grid),
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT>), dim3(grid),
                        dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr, b.n, ppr, 0u,
                        (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
     hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
                        part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  flat2 r=%d  round (2 launches) %8.4f ms %7.1f GB/s\n", R, flat,
-              bytes / (flat * 1e-3) / 1e9);
+  std::printf("  flat2 r=%d nt=%d alt=%d  round (2 launches) %8.4f ms %7.1f GB/s\n",
+              R, (int)NT, (int)ALT, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
 template <typename T>
@@ -304,9 +304,11 @@ run(unsigned nr, unsigned n)
     HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
     const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
     round_ref<T>(b, big ? 2 : (b.n > 12288 ? 2 : 4), big ? 256 : 256);
-    flat_seq<T, 1, 2, false>(b, part);
     flat2_seq<T, 2>(b, part);
-    flat2_seq<T, 4>(b, part);
+    flat2_seq<T, 2, true, true>(b, part);
+    flat2_seq<T, 2, false, false>(b, part);
+    flat2_seq<T, 2, false, true>(b, part);
+    flat2_seq<T, 4, false, true>(b, part);
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
     HIPCHECK(hipFree(b.s));
