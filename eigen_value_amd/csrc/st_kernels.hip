@@ -99,10 +99,13 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   return { 4, true, 512u };
 }
 
-// the flat round (k_flat + k_parts) for blocks of >= 1 GiB:
-// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat2.log (32768^2
-// fp64 2.72 ms vs 3.05 for k_round; 16384^2 0.68 vs 0.77; below 1 GiB the
-// cached k_round, which the MALL helps, stays ahead)
+// the flat round (k_flat + k_parts) for blocks of >= 288 MiB, with cached
+// accesses and alternating piece order below 2 GiB (the memory-side cache
+// then serves the start of each round) and non-temporal ones above:
+// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat_cached.log
+// (32768^2 fp64 2.72 ms vs 3.06 for k_round; 16384^2 0.68 vs 0.76; 8192^2
+// 0.163 vs 0.168; the 2880x23040 block 0.168 vs 0.184; at 256 MiB and
+// below k_round stays ahead)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
 // than in a k_stats launch of their own (three)
@@ -111,7 +114,13 @@ constexpr bool kFlatFusedStats = true;
 inline bool
 flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  return block_bytes(nrows, ncols, elem) >= ((size_t)1 << 30);
+  return block_bytes(nrows, ncols, elem) >= ((size_t)288 << 20);
+}
+
+inline bool
+flat_round_nt(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return block_bytes(nrows, ncols, elem) >= ((size_t)2 << 30);
 }
 
 // partial sums per row (one per piece) and the scratch they need
@@ -434,7 +443,7 @@ launch_round_split(int span, T* a, const T* s_cur, T* s_next, T* part, T* v,
   return check_launch("round_split");
 }
 
-template <typename T, int W, int ORDER>
+template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                   uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
@@ -448,7 +457,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, true, kFlatRows, false, true>), dim3(grid),
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, true>), dim3(grid),
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
       st, eps, max_itr, semantics);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
@@ -459,9 +468,9 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, true, kFlatRows, false>), dim3(grid),
-      dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
-      st, eps, max_itr, semantics);
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, true>),
+      dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols,
+      ppr, row0, k, st, eps, max_itr, semantics);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, nullptr, nullptr, 0u);
   }
@@ -490,20 +499,23 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
   constexpr int W = 16 / sizeof(T);
   const bool vec_ok = (ncols % W) == 0 && aligned16(a) && aligned16(s_cur);
   const bool order1 = semantics == ST_SEM_MAINPY;
-  if (vec_ok)
-    order1 ? launch_flat_parts<T, W, 1>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, eps, k, max_itr,
-                                        semantics, st, stream)
-           : launch_flat_parts<T, W, 0>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, eps, k, max_itr,
-                                        semantics, st, stream);
-  else
-    order1 ? launch_flat_parts<T, 1, 1>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, eps, k, max_itr,
-                                        semantics, st, stream)
-           : launch_flat_parts<T, 1, 0>(a, s_cur, s_next, part, v, nrows,
-                                        ncols, row0, eps, k, max_itr,
-                                        semantics, st, stream);
+  const bool nt = flat_round_nt(nrows, ncols, sizeof(T));
+#define ST_FLAT(WW, OO, NN)                                                    \
+  launch_flat_parts<T, WW, OO, NN>(a, s_cur, s_next, part, v, nrows, ncols,    \
+                                   row0, eps, k, max_itr, semantics, st,       \
+                                   stream)
+  if (vec_ok) {
+    if (order1)
+      nt ? ST_FLAT(W, 1, true) : ST_FLAT(W, 1, false);
+    else
+      nt ? ST_FLAT(W, 0, true) : ST_FLAT(W, 0, false);
+  } else {
+    if (order1)
+      nt ? ST_FLAT(1, 1, true) : ST_FLAT(1, 1, false);
+    else
+      nt ? ST_FLAT(1, 0, true) : ST_FLAT(1, 0, false);
+  }
+#undef ST_FLAT
   return check_launch("round_flat");
 }
 
