@@ -143,7 +143,7 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   const T eps = (T)eps_d;
   const uint32_t max_itr = (opt && opt->max_itr) ? opt->max_itr : ST_MAX_ITR;
   const uint32_t sem = opt ? opt->semantics : ST_SEM_SYCL;
-  const uint32_t batch = (opt && opt->batch) ? opt->batch : 8u;
+  uint32_t batch = (opt && opt->batch) ? opt->batch : 0u;
   const bool mfree = opt && (opt->flags & ST_FLAG_MATRIX_FREE);
   ST_REQUIRE(sem <= ST_SEM_MAINPY, "unknown semantics %u", sem);
 
@@ -202,6 +202,8 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   ST_CHECK(hipHostMalloc(&M.h_state, 2 * sizeof(st_state), hipHostMallocDefault));
   ST_CHECK(hipEventCreateWithFlags(&M.ev[0], hipEventDisableTiming));
   ST_CHECK(hipEventCreateWithFlags(&M.ev[1], hipEventDisableTiming));
+  if (batch == 0) // as st_solve.hip: flat rounds are checked every 2 rounds
+    batch = M.sh[0].part ? 2u : 8u;
   {
     std::vector<ncclComm_t> comms(P);
     ST_NCCL(ncclCommInitAll(comms.data(), (int)P, devlist.data()));

@@ -53,6 +53,7 @@ clear_error()
 namespace {
 
 constexpr uint32_t kDefaultBatch = 8;
+constexpr uint32_t kFlatBatch = 2;
 
 struct Context
 {
@@ -163,7 +164,7 @@ resolve(const st_options* opt, Resolved* r)
   r->eps = (opt && opt->eps >= 0.0) ? opt->eps : (double)default_eps<T>();
   r->max_itr = (opt && opt->max_itr) ? opt->max_itr : ST_MAX_ITR;
   r->semantics = opt ? opt->semantics : ST_SEM_SYCL;
-  r->batch = (opt && opt->batch) ? opt->batch : kDefaultBatch;
+  r->batch = (opt && opt->batch) ? opt->batch : 0; // 0: per round form
   r->flags = opt ? opt->flags : 0u;
   ST_REQUIRE(r->semantics <= ST_SEM_MAINPY, "unknown semantics %u",
              r->semantics);
@@ -202,6 +203,12 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   if (flat && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
     return -1;
   T* d_part = reinterpret_cast<T*>(c->d_part);
+  // rounds per host flag check: the launches queued behind the stopping
+  // round still run as gated no-ops, and a gated flat round is two launches
+  // of up to millions of workgroups (~10 us each), so the flat form checks
+  // every 2 rounds (>= 0.16 ms of work each) and the one-launch form every 8
+  if (o.batch == 0)
+    o.batch = flat ? kFlatBatch : kDefaultBatch;
   // timing events [rowsum_a, rowsum_b, (round_a, round_b)*], destroyed on
   // every exit path
   struct Events
