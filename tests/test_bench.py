@@ -22,8 +22,10 @@ def test_weak_scaled_sizes():
 
 
 def test_committed_measurements_are_found():
-    tr = bench.load_traffic("hilbert8192_f64")
+    tr = bench.load_traffic("hilbert8192_f64", "k_flat")
     assert tr is not None and abs(tr[0] / (2 * 8192**2 * 8) - 1) < 0.01
+    tr = bench.load_traffic("random32768_f64", "k_flat")
+    assert tr is not None and abs(tr[0] / (2 * 32768**2 * 8) - 1) < 0.01
     tr = bench.load_traffic("random32768_f64", "k_mfree")
     assert tr is not None and abs(tr[0] / (32768**2 * 8) - 1) < 0.01
     assert bench.load_traffic("no_such_workload") is None
