@@ -248,7 +248,9 @@ def main():
                            else "k_round (fused stats + scale + row-sum)"),
                 "fused_ms_avg": round(fused_ms, 5),
                 "bytes_per_launch": bytes_round_local,
-                "timing": ("HIP events bracketing the K timed launches on the launch stream"
+                "timing": ("HIP events bracketing the K timed rounds on the launch stream"
+                           + ("; a round is k_flat + k_parts: compare with the sum of their "
+                              "rocprof averages (profiles/*_kernel_stats.csv)" if flat else "")
                            if world == 1 else
                            "HIP events around every launch of a 50-round pass after the timed region"),
                 "traffic_source": None if traffic is None else traffic[1]}
