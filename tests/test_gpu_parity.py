@@ -321,16 +321,18 @@ def _gpu_gloo_worker(rank, world, port, n, outdir, overlap=False):
         dist.destroy_process_group()
 
 
-def test_sharded_two_ranks_on_one_gpu(tmp_path, solver):
+@pytest.mark.parametrize("n", [2501, 9216])
+def test_sharded_two_ranks_on_one_gpu(tmp_path, solver, n):
     """The row-block path with P = 2 (both ranks on cuda:0, gloo exchange)
     gives bitwise the single-GPU result: per-row sums do not depend on the
-    partition and every rank derives identical m_k / stop_k."""
+    partition and every rank derives identical m_k / stop_k.  2501: ragged
+    blocks on k_round; 9216: 324 MiB blocks on the flat round (and 648 MiB
+    single-GPU, also flat)."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    n = 2501                                   # ragged: 1251 + 1250 rows
     mp.spawn(_gpu_gloo_worker, args=(2, port, n, str(tmp_path)), nprocs=2, join=True)
     a = dev.generate("random", n, torch.float64, seed=6, device=DEV)
     lam, v, it, st = solver.solve(a)
