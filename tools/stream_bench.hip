@@ -297,6 +297,18 @@ main(int argc, char** argv)
     B.grids<256, 2, 0, 2>();
     return 0;
   }
+  if (std::getenv("STREAM_FLAT_BLK")) { // flat in-place: workgroup size
+    B.runflat<64, 1, 1, 0>();
+    B.runflat<128, 1, 1, 0>();
+    B.runflat<256, 1, 1, 0>();
+    B.runflat<512, 1, 1, 0>();
+    B.runflat<64, 2, 1, 0>();
+    B.runflat<128, 2, 1, 0>();
+    B.runflat<64, 1, 0, 0>();
+    B.runflat<128, 1, 0, 0>();
+    B.runflat<256, 1, 0, 0>();
+    return 0;
+  }
   if (std::getenv("STREAM_FLAT")) { // babelstream-style flat dispatch only
     B.runflat<256, 1, 0, 0>();
     B.runflat<256, 1, 1, 0>();

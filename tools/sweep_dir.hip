@@ -184,23 +184,23 @@ flat_seq(const Bufs<T>& b, T* part)
 
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
-template <typename T, int R, bool NT = true, bool ALT = false>
+template <typename T, int R, bool NT = true, bool ALT = false, int FB = 256>
 static void
 flat2_seq(const Bufs<T>& b, T* part)
 {
   constexpr int W = 16 / sizeof(T);
-  const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
+  const unsigned ppr = (b.n + FB * W - 1) / (FB * W);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   float flat = time_seq([&](int k) {
-    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT>), dim3(grid),
-                       dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr, b.n, ppr, 0u,
-                       (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB>),
+                       dim3(grid), dim3(FB), 0, 0, b.a, b.s, part, b.v, b.nr,
+                       b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
     hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
                        part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  flat2 r=%d nt=%d alt=%d  round (2 launches) %8.4f ms %7.1f GB/s\n",
-              R, (int)NT, (int)ALT, flat, bytes / (flat * 1e-3) / 1e9);
+  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d  round (2 launches) %8.4f ms %7.1f GB/s\n",
+              R, (int)NT, (int)ALT, FB, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
 template <typename T>
@@ -300,15 +300,21 @@ run(unsigned nr, unsigned n)
   stream_seq<T, false>(b, true);
   if (std::getenv("SWEEP_FLAT")) { // the flat round vs k_round
     T* part = nullptr;
-    const unsigned ppr = (b.n + 255) / 256;
+    const unsigned ppr = (b.n + 63) / 64;
     HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
     const bool big = nn * sizeof(T) >= ((size_t)1 << 30);
     round_ref<T>(b, big ? 2 : (b.n > 12288 ? 2 : 4), big ? 256 : 256);
-    flat2_seq<T, 2>(b, part);
-    flat2_seq<T, 2, true, true>(b, part);
-    flat2_seq<T, 2, false, false>(b, part);
-    flat2_seq<T, 2, false, true>(b, part);
-    flat2_seq<T, 4, false, true>(b, part);
+    if (big) {
+      flat2_seq<T, 2, true, true>(b, part);
+      flat2_seq<T, 2, true, true, 64>(b, part);
+      flat2_seq<T, 4, true, true, 64>(b, part);
+      flat2_seq<T, 2, true, true, 128>(b, part);
+    } else {
+      flat2_seq<T, 2, false, true>(b, part);
+      flat2_seq<T, 2, false, true, 64>(b, part);
+      flat2_seq<T, 4, false, true, 64>(b, part);
+      flat2_seq<T, 2, false, true, 128>(b, part);
+    }
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
     HIPCHECK(hipFree(b.s));
