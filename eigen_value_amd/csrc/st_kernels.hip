@@ -51,8 +51,13 @@ check_launch(const char* what)
 //     L2) and walks them backwards on odd rounds (ALT in st_device.h), so a
 //     round starts on the rows the previous round touched last;
 //   * k_round: 4 rows per group while rows are short (<= 96 KiB streamed,
-//     <= 12288 columns cached), 2 above; one workgroup per CU; 1 row per group and 2 workgroups per CU below 1024 rows.
-//   * k_mfree: 4 rows per group, 2 workgroups per CU (2 rows below 512 MiB).
+//     <= 12288 columns cached), 2 above; one workgroup per CU; 2 rows and
+//     2 (<= 128 MiB) or 4 (<= 32 MiB) workgroups per CU on small matrices;
+//     1 row per group below 1024 rows.  (The solve loops hand blocks of
+//     288 MiB and more to the flat round below; st_round_* keeps these
+//     shapes at every size.)
+//   * k_mfree: 4 rows per group, 2 workgroups per CU (2 rows between 64
+//     and 512 MiB).
 constexpr int kRows = 2; // k_fused (K0 row sums and the step API)
 constexpr int kUnroll = 2;
 constexpr uint32_t kGridCap = 512;
