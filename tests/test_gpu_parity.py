@@ -779,6 +779,20 @@ def test_native_multi_gpu_solve(orc, matrix_free):
         solve_multi(1, "hilbert", devices=[0, 0])
 
 
+def test_native_multi_gpu_flat_round(solver):
+    """st_solve_multi_* on a block that takes the flat round (9216², 648 MiB)
+    equals the library's single-GPU solve loop bit for bit."""
+    from eigen_value_amd.multi import solve_multi
+    n = 9216
+    lam, v, it, st = solve_multi(n, "random", ngpus=1, seed=3)
+    a = dev.generate("random", n, torch.float64, seed=3, device=DEV)
+    lam1, v1, it1, st1 = solver.solve(a, inplace=True)
+    assert lam == lam1 and it == it1 and st["rounds"] == st1["rounds"]
+    assert np.array_equal(v, to_np(v1))
+    del a
+    torch.cuda.empty_cache()
+
+
 def test_fuzz_vs_oracle(eigen, orc):
     """Seeded random sweep over size, dtype, semantics, form, batch and
     eps: iteration counts equal to the oracle's, λ / v within the dtype's
