@@ -114,6 +114,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.max_eigen_value_f64.restype = i64
     L.max_eigen_value_ex.argtypes = [P, i32, P, P, P, u32, P, P, P]
     L.max_eigen_value_ex.restype = i64
+    L.st_last_round_times.argtypes = [P, P, u32]
+    L.st_last_round_times.restype = i32
     L.st_set_stream.argtypes = [P, P]
     L.st_set_stream.restype = i32
     L.st_use_own_stream.argtypes = [P]

@@ -69,6 +69,7 @@ struct Context
   size_t part_bytes = 0;
   st_state* d_state = nullptr;
   st_state* h_state = nullptr; // pinned, 2 slots
+  std::vector<float> round_ms; // per-round kernel time of the last timed solve
   hipEvent_t ev_flag[2] = { nullptr, nullptr };
 };
 
@@ -306,6 +307,20 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
                        hipMemcpyDeviceToHost));
   const double d2h_ms = ms_since(t1);
 
+  // per-round kernel times (rounds 0 .. end-1 did work; the stop round's
+  // launch also streams the matrix), kept for st_last_round_times
+  c->round_ms.clear();
+  float rowsum_ms = 0.f;
+  double tot = 0.0;
+  if (timed) {
+    (void)hipEventElapsedTime(&rowsum_ms, ev[0], ev[1]);
+    for (uint32_t k = 0; k < fin.end && 2 + 2 * k + 1 < ev.size(); k++) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[2 + 2 * k], ev[2 + 2 * k + 1]);
+      c->round_ms.push_back(ms);
+      tot += ms;
+    }
+  }
   if (stats) {
     std::memset(stats, 0, sizeof(*stats));
     stats->loop_ms = loop_ms;
@@ -313,19 +328,9 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     stats->rounds = fin.end;
     stats->converged = fin.stop;
     if (timed) {
-      float ms = 0.f;
-      (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
-      stats->rowsum_ms = ms;
-      // round launches that did work: rounds 0 .. end-1 (the stop round's
-      // launch also streams the matrix)
-      uint32_t transforms = fin.end;
-      double tot = 0.0;
-      for (uint32_t k = 0; k < transforms && 2 + 2 * k + 1 < ev.size(); k++) {
-        (void)hipEventElapsedTime(&ms, ev[2 + 2 * k], ev[2 + 2 * k + 1]);
-        tot += ms;
-      }
+      stats->rowsum_ms = rowsum_ms;
       stats->fused_ms_total = tot;
-      stats->fused_launches = transforms;
+      stats->fused_launches = (uint32_t)c->round_ms.size();
     }
   }
   return (int64_t)loop_ms;
@@ -460,6 +465,19 @@ destroy_queue(void* wq)
   if (c->own_stream)
     (void)hipStreamDestroy(c->own_stream);
   delete c;
+}
+
+int
+st_last_round_times(void* wq, float* ms, unsigned int cap)
+{
+  st::clear_error();
+  Context* c = st::as_ctx(wq);
+  ST_REQUIRE(c, "st_last_round_times: null queue");
+  ST_REQUIRE(ms || cap == 0, "st_last_round_times: null buffer");
+  const size_t n = c->round_ms.size();
+  for (size_t i = 0; i < n && i < cap; i++)
+    ms[i] = c->round_ms[i];
+  return (int)n;
 }
 
 int

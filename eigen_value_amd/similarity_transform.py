@@ -100,6 +100,17 @@ class EigenValue:
         _lib.check(ts, "max_eigen_value_ex")
         return eigen_val[0], eigen_vec, int(ts), int(iter_cnt[0]), stats.as_dict()
 
+    def last_round_times(self) -> np.ndarray:
+        """Per-round kernel times (ms) of the last ``similarity_transform_ex``
+        call made with ``time_kernels=True`` (empty otherwise)."""
+        n = _lib.check(self.so_lib.st_last_round_times(self.sycl_q, None, 0),
+                       "st_last_round_times")
+        out = np.zeros(n, dtype=np.float32)
+        if n:
+            _lib.check(self.so_lib.st_last_round_times(self.sycl_q, out.ctypes.data, n),
+                       "st_last_round_times")
+        return out
+
     # ------------------------------------------------------------------
     def close(self) -> None:
         if self.so_lib is not None and self.sycl_q is not None and self.sycl_q.value:

@@ -111,6 +111,12 @@ int64_t max_eigen_value_ex(void* wq, int dtype, const void* mat,
                            unsigned int dim, unsigned int* iter_cnt,
                            const st_options* opt, st_stats* stats);
 
+/* Per-round kernel times (ms) of the last solve on this queue that ran
+ * with ST_FLAG_TIME_KERNELS: copies min(cap, n) values into ms and returns
+ * n, the number of rounds that did work (0 if the last solve was not
+ * timed), or a negative value on error. */
+int st_last_round_times(void* wq, float* ms, unsigned int cap);
+
 /* Make the context launch on a caller stream (a hipStream_t; NULL is the
  * HIP null stream, which is torch's default stream).  Returns 0 or
  * negative.  st_use_own_stream restores the context's own non-blocking

@@ -503,6 +503,11 @@ def test_batch_size_does_not_change_results(eigen, orc, batch):
     lam, v, ts, itr, st = eigen.similarity_transform_ex(mat, batch=batch, time_kernels=True)
     assert lam == base[0] and np.array_equal(v, base[1]) and itr == base[3] == 12
     assert st["fused_launches"] == itr + 1 and st["fused_ms_total"] > 0  # rounds 0..itr
+    rt = eigen.last_round_times()                      # per-round times of that solve
+    assert rt.size == itr + 1 and np.all(rt > 0)
+    assert abs(rt.sum() - st["fused_ms_total"]) <= 1e-3 * st["fused_ms_total"] + 1e-6
+    eigen.similarity_transform(mat)                     # untimed solve clears them
+    assert eigen.last_round_times().size == 0
 
 
 def test_device_solver(solver, orc):
