@@ -404,6 +404,28 @@ def main():
                                "solve_ms": round(solve_cpu.loop_ms, 2),
                                "solve_iter_count": solve_cpu.iter_count}
         out["speedup_vs_cpu"] = round(out["ms_per_step"] and per_round_ms / out["ms_per_step"], 1)
+        # configs[0]: 128x128 Hilbert on the CPU path:
+        # the C restatement on one core (fp64 / fp32, the SYCL loop), a numpy
+        # restatement of main.py's loop, eigenvalues against eigvalsh
+        h64 = orc.hilbert(128)
+        true128 = float(np.max(np.linalg.eigvalsh(h64)))
+        c64 = orc.similarity_transform(h64, orc.SEM_SYCL, nthreads=1)
+        c32 = orc.similarity_transform(orc.hilbert(128, np.float32), orc.SEM_SYCL, nthreads=1)
+        t0 = time.perf_counter()
+        a, v, itr = h64.copy(), np.ones(128), 0
+        for itr in range(1000):          # main.py:30-47, elementwise (no O(N^3) matmul)
+            s_ = a.sum(axis=1)
+            v = v * (s_ / s_.max())
+            if np.all(np.abs(np.diff(s_)) < 1e-3):
+                break
+            a = (a / s_[:, None]) * s_[None, :]
+        np_ms = (time.perf_counter() - t0) * 1e3
+        out["cpu_baseline"]["config1_hilbert128"] = {
+            "c_1core_f64": {"ms": round(c64.loop_ms, 4), "iter_count": c64.iter_count,
+                            "rel_err_vs_eigvalsh": abs(c64.eigen_val - true128) / true128},
+            "c_1core_f32": {"ms": round(c32.loop_ms, 4), "iter_count": c32.iter_count},
+            "numpy_mainpy_semantics": {"ms": round(np_ms, 3), "iter_count": itr + 1,
+                                       "eigen_val": float(s_[0])}}
 
     if rank == 0:
         print(json.dumps(out), flush=True)
