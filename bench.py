@@ -238,12 +238,15 @@ def main():
     bytes_round_local = 2.0 * p.nrows * n * b
     value = bytes_round_total * args.steps / el / 1e9
     achieved = bytes_round_local / (fused_ms * 1e-3) / 1e9
-    flat = (not args.overlap) and dev.flat_round_pays(p.nrows, n, dt)
+    flat_pays = dev.flat_round_pays(p.nrows, n, dt)
+    flat = (not args.overlap) and flat_pays
     traffic = load_traffic(workload, "k_flat" if flat else "k_round")
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic[0],
-                "kernel": ("k_round_split local + remote (overlapped exchange)" if args.overlap
+                "kernel": (("flat split: k_flat local + k_flat remote + k_parts" if flat_pays
+                            else "k_round_split local + remote") + " (overlapped exchange)"
+                           if args.overlap
                            else "flat round: k_flat + k_parts" if flat
                            else "k_round (fused stats + scale + row-sum)"),
                 "fused_ms_avg": round(fused_ms, 5),

@@ -140,14 +140,19 @@ def _declare(L: ctypes.CDLL) -> None:
                                                         u32, u32, P, P]
         getattr(L, f"st_round_split_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, u32,
                                                         u32, T, u32, u32, u32, i32, P, P]
+        getattr(L, f"st_round_split_flat_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32,
+                                                             u32, u32, T, u32, u32, u32,
+                                                             i32, P, P]
         getattr(L, f"st_round_flat_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, T, u32,
                                                        u32, u32, P, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
                      "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round",
-                     "round_split", "round_flat"):
+                     "round_split", "round_split_flat", "round_flat"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
     L.st_round_flat_scratch.argtypes = [u32, u32]
     L.st_round_flat_scratch.restype = u64
+    L.st_round_split_flat_scratch.argtypes = [u32, u32, u32, u32]
+    L.st_round_split_flat_scratch.restype = u64
     L.st_round_flat_pays.argtypes = [u32, u32, i32]
     L.st_round_flat_pays.restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]

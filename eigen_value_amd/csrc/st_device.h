@@ -667,14 +667,33 @@ k_stats(const T* __restrict__ s, uint32_t n, T eps, uint32_t k,
   }
 }
 
+// The pieces (PWC columns each, ppr per row) lying wholly inside the local
+// column range [col0, col1) of a split round: [pa, pa + nfull).  The piece
+// past ncols' end counts as inside when col1 == ncols.
+template <uint32_t PWC>
+__host__ __device__ inline void
+split_full_pieces(uint32_t ncols, uint32_t ppr, uint32_t col0, uint32_t col1,
+                  uint32_t& pa, uint32_t& nfull)
+{
+  pa = (col0 + PWC - 1) / PWC;
+  const uint32_t pb = col1 >= ncols ? ppr : col1 / PWC;
+  nfull = pb > pa ? pb - pa : 0u;
+}
+
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          bool FS = false, bool ALT = false, int BLK = kBlock>
+          bool FS = false, bool ALT = false, int BLK = kBlock, int SPLIT = 0>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
-       uint32_t max_itr = 0, uint32_t semantics = 0)
+       uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
+       uint32_t col0 = 0, uint32_t col1 = 0)
 {
+  // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
+  // columns [col0, col1) whose scales this rank computed itself, over the
+  // ppr pieces starting at piece p_lo (no stats, no v update); 2 = every
+  // other column of all pieces (with the stats when FS).  Lanes outside
+  // their half are idle; col0 and col1 are multiples of W.
   // ALT: odd rounds walk the pieces from the end of the matrix, so a round
   // starts where the previous one finished (memory-side cache reuse)
   // FS: the first row group's workgroups (pieces 0..ppr-1, together all of
@@ -693,14 +712,32 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   constexpr int NW = BLK / 64;
   __shared__ T red[NW][R];
   const uint32_t b = (ALT && (k & 1u)) ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
-  const uint32_t rg = b / ppr;
-  const uint32_t p = b - rg * ppr;
-  const uint32_t c = (p * BLK + threadIdx.x) * W;
+  uint32_t rg, p;                                  // p: index into this row's parts
+  if constexpr (SPLIT == 2) {
+    // the pieces wholly inside [col0, col1) have nothing to do past row
+    // group 0 (which takes the stats over every piece): the grid skips them
+    uint32_t pa, nfull;
+    split_full_pieces<BLK * W>(ncols, ppr, col0, col1, pa, nfull);
+    if (b < ppr) {
+      rg = 0;
+      p = b;
+    } else {
+      const uint32_t pr = ppr - nfull, bb = b - ppr;
+      rg = 1 + bb / pr;
+      const uint32_t q = bb - (rg - 1) * pr;
+      p = q < pa ? q : q + nfull;
+    }
+  } else {
+    rg = b / ppr;
+    p = b - rg * ppr;
+  }
+  const uint32_t c = ((SPLIT == 1 ? p_lo + p : p) * BLK + threadIdx.x) * W;
   const uint32_t r0 = rg * R;
   T acc[R];
   V x[R];
   T sr[R];
-  const bool in = c < ncols; // ncols % W == 0 on the vector path (host-checked)
+  const bool in_cols = c < ncols; // ncols % W == 0 on the vector path
+  const bool in = in_cols && (SPLIT == 0 || ((c >= col0 && c < col1) == (SPLIT == 1)));
 #pragma unroll
   for (int j = 0; j < R; j++) {
     acc[j] = (T)0;
@@ -713,7 +750,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       __shared__ T mx_sh[NW];
       T mx = (T)0;
       int ok = 1;
-      if (in) {
+      if (in_cols) {
         const V sc0 = *reinterpret_cast<const V*>(s_cur + c);
         stats_at<T, W>(s_cur, sc0, c / W, ncols, semantics == ST_SEM_SYCL, eps,
                        mx, ok);
@@ -748,7 +785,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       }
     }
   }
-  if (!FS && p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
+  if (!FS && SPLIT == 0 && p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
     // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats
     const uint32_t r = row0 + r0 + threadIdx.x;
     const T m = (T)state->max;
@@ -782,8 +819,11 @@ __global__ __launch_bounds__(BLK) void
 k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
         uint32_t ppr /* partials per row */, uint32_t k, const st_state* state,
         const T* __restrict__ s_cur = nullptr, T* __restrict__ v = nullptr,
-        uint32_t row0 = 0)
+        uint32_t row0 = 0, const T* __restrict__ part2 = nullptr,
+        uint32_t ppr2 = 0, uint32_t skip0 = 0, uint32_t nskip = 0)
 {
+  // [skip0, skip0 + nskip): parts of `part` not written (split round)
+  // part2 (split round): the local half's partials, added after part's
   // v != nullptr: also v[r] *= s_k[r] / m_k (cpp:260) with m_k published by
   // k_flat's first row group
   {
@@ -799,8 +839,16 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   const T* row = part + (size_t)r * ppr;
   T acc = (T)0;
   for (uint32_t p = lane; p < ppr; p += 64)
-    acc += row[p];
+    if (p - skip0 >= nskip)
+      acc += row[p];
   acc = wave_sum(acc);
+  if (part2 != nullptr) {
+    const T* row2 = part2 + (size_t)r * ppr2;
+    T acc2 = (T)0;
+    for (uint32_t p = lane; p < ppr2; p += 64)
+      acc2 += row2[p];
+    acc += wave_sum(acc2);
+  }
   if (lane == 0) {
     s_next[r] = acc;
     if (v != nullptr) {

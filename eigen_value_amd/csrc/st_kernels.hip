@@ -524,6 +524,128 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
   return check_launch("round_flat");
 }
 
+// ---- the flat round split in two for the overlapped exchange ------------
+// span 1 (local): k_flat over the pieces holding [col0, col1), lanes masked
+// to those columns, partials to the local region of `part`; span 2
+// (remote): k_flat over every piece with the other columns and the fused
+// stats, then k_parts sums remote-then-local partials (fixed order: the
+// result does not depend on how the two launches interleave with the
+// all-gather) and updates v.  `part` holds split_flat_scratch() elements:
+// [nrows x flat_pieces(ncols, 1)] remote, then the local region.
+inline size_t
+split_flat_local_off(uint32_t nrows, uint32_t ncols)
+{
+  return flat_scratch_elems(nrows, ncols);
+}
+
+inline size_t
+split_flat_scratch_elems(uint32_t nrows, uint32_t ncols, uint32_t col0,
+                         uint32_t col1)
+{
+  return split_flat_local_off(nrows, ncols) +
+         (size_t)nrows * (flat_pieces(col1 - col0, 1) + 1);
+}
+
+template <typename T, int W, int ORDER, bool NT>
+void
+launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
+                      T* v, uint32_t nrows, uint32_t ncols, uint32_t row0,
+                      uint32_t col0, uint32_t col1, T eps, uint32_t k,
+                      uint32_t max_itr, uint32_t semantics, st_state* st,
+                      hipStream_t stream)
+{
+  constexpr uint32_t PW = kBlock * W;
+  const uint32_t ppr = flat_pieces(ncols, W);
+  const uint32_t p_lo = col0 / PW;
+  const uint32_t npl = col1 > col0 ? (col1 + PW - 1) / PW - p_lo : 0u;
+  const uint32_t ngroups = (nrows + kFlatRows - 1) / kFlatRows;
+  T* part_local = part + split_flat_local_off(nrows, ncols);
+  if (span == 1) {
+    if (npl == 0)
+      return;
+    // a local half short of the whole row streams non-temporally at every
+    // size: cached, it would evict from the MALL what the remote half is
+    // about to re-read (profiles/r01_split_cost.log)
+    if (NT || col1 - col0 < ncols)
+      hipLaunchKernelGGL(
+        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, true, kBlock, 1>),
+        dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
+        nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
+        col1);
+    else
+      hipLaunchKernelGGL(
+        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, true, kBlock, 1>),
+        dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
+        nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
+        col1);
+    return;
+  }
+  // row group 0 over every piece (it takes the stats), the other row
+  // groups only over pieces holding remote columns
+  uint32_t pa, nfull;
+  dev::split_full_pieces<PW>(ncols, ppr, col0, col1, pa, nfull);
+  hipLaunchKernelGGL(
+    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, true, kBlock, 2>),
+    dim3(ppr + (ngroups - 1) * (ppr - nfull)), dim3(kBlock), 0, stream, a,
+    s_cur, part, v, nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
+    0u, col0, col1);
+  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
+  hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
+                     part, s_next, nrows, ppr, k, st, s_cur, v, row0,
+                     (const T*)part_local, npl, pa, nfull);
+}
+
+template <typename T>
+int
+launch_round_split_flat(int span, T* a, const T* s_cur, T* s_next, T* part,
+                        T* v, uint32_t nrows, uint32_t ncols, uint32_t row0,
+                        uint32_t col0, uint32_t col1, T eps, uint32_t k,
+                        uint32_t max_itr, uint32_t semantics, st_state* st,
+                        hipStream_t stream)
+{
+  ST_REQUIRE(a && s_cur && part && st, "round_split_flat: null pointer");
+  ST_REQUIRE(span == 1 || span == 2, "round_split_flat: span must be 1 "
+                                     "(local) or 2 (remote), not %d", span);
+  ST_REQUIRE(span == 1 || (s_next && v), "round_split_flat: null pointer");
+  ST_REQUIRE(ncols > 0 && nrows > 0, "round_split_flat: empty block");
+  ST_REQUIRE(row0 + (uint64_t)nrows <= ncols,
+             "round_split_flat: rows [%u, %u) outside the %u-long row-sum "
+             "vector", row0, row0 + nrows, ncols);
+  ST_REQUIRE(col0 <= col1 && col1 <= ncols,
+             "round_split_flat: bad local column range [%u, %u) of %u", col0,
+             col1, ncols);
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "round_split_flat: bad semantics %u",
+             semantics);
+  ST_REQUIRE(max_itr > 0, "round_split_flat: max_itr must be > 0");
+  ST_REQUIRE((uint64_t)((nrows + kFlatRows - 1) / kFlatRows) *
+                 flat_pieces(ncols, 1) <
+               (1ull << 31),
+             "round_split_flat: %u x %u is too large for one launch", nrows,
+             ncols);
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && (col0 % W) == 0 && (col1 % W) == 0 &&
+                      aligned16(a) && aligned16(s_cur);
+  const bool order1 = semantics == ST_SEM_MAINPY;
+  const bool nt = flat_round_nt(nrows, ncols, sizeof(T));
+#define ST_SFLAT(WW, OO, NN)                                                   \
+  launch_split_flat_cfg<T, WW, OO, NN>(span, a, s_cur, s_next, part, v, nrows, \
+                                       ncols, row0, col0, col1, eps, k,        \
+                                       max_itr, semantics, st, stream)
+  if (vec_ok) {
+    if (order1)
+      nt ? ST_SFLAT(W, 1, true) : ST_SFLAT(W, 1, false);
+    else
+      nt ? ST_SFLAT(W, 0, true) : ST_SFLAT(W, 0, false);
+  } else {
+    if (order1)
+      nt ? ST_SFLAT(1, 1, true) : ST_SFLAT(1, 1, false);
+    else
+      nt ? ST_SFLAT(1, 0, true) : ST_SFLAT(1, 0, false);
+  }
+#undef ST_SFLAT
+  return check_launch("round_split_flat");
+}
+
 size_t
 round_flat_scratch(uint32_t nrows, uint32_t ncols)
 {
@@ -768,6 +890,19 @@ st_state_reset(st_state* d_state, void* stream)
                                      k, max_itr, semantics, d_state,           \
                                      ST_STREAM(stream));                       \
   }                                                                            \
+  int st_round_split_flat_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,      \
+                                T* d_part, T* d_v, unsigned int nrows,         \
+                                unsigned int ncols, unsigned int row0,         \
+                                unsigned int col0, unsigned int col1, T eps,   \
+                                unsigned int k, unsigned int max_itr,          \
+                                unsigned int semantics, int span,              \
+                                st_state* d_state, void* stream)               \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_round_split_flat<T>(                                     \
+      span, d_mat, d_s_cur, d_s_next, d_part, d_v, nrows, ncols, row0, col0,   \
+      col1, eps, k, max_itr, semantics, d_state, ST_STREAM(stream));           \
+  }                                                                            \
   int st_mfree_round_##SFX(const T* d_mat0, const T* d_s_prev, T* d_s_next,    \
                            const T* d_v_prev, T* d_v_cur, unsigned int nrows,  \
                            unsigned int ncols, unsigned int row0, T eps,       \
@@ -796,6 +931,15 @@ uint64_t
 st_round_flat_scratch(unsigned int nrows, unsigned int ncols)
 {
   return st::round_flat_scratch(nrows, ncols);
+}
+
+uint64_t
+st_round_split_flat_scratch(unsigned int nrows, unsigned int ncols,
+                            unsigned int col0, unsigned int col1)
+{
+  if (col1 < col0)
+    return 0;
+  return st::split_flat_scratch_elems(nrows, ncols, col0, col1);
 }
 
 int

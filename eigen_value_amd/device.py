@@ -212,6 +212,33 @@ def split_round(mat, s_cur, s_next, part, v, state, *, span: int, row0: int = 0,
         _stream(mat.device)), "round_split")
 
 
+def split_flat_scratch(nrows: int, ncols: int, col0: int, col1: int, dtype, device=None):
+    """Partial-sum scratch for split_flat_round on this block and local range."""
+    torch = _torch()
+    n = int(_lib.load().st_round_split_flat_scratch(nrows, ncols, col0, col1))
+    return torch.empty(n, dtype=dtype, device=device or "cuda")
+
+
+def split_flat_round(mat, s_cur, s_next, part, v, state, *, span: int, row0: int = 0,
+                     col0: int = 0, col1: Optional[int] = None, eps: float = 1e-3,
+                     k: int = 0, max_itr: int = _lib.ST_MAX_ITR,
+                     semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """split_round in the flat form (st_round_split_flat): ``part`` is the
+    split_flat_scratch of this block and range, shared by both halves."""
+    _check_cuda(mat, s_cur, s_next, part, v, state)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    col1 = ncols if col1 is None else col1
+    need = int(_lib.load().st_round_split_flat_scratch(nrows, ncols, col0, col1))
+    assert s_cur.numel() >= ncols and part.numel() >= need and row0 + nrows <= ncols
+    assert span == SPAN_LOCAL or (s_next is not None and s_next.numel() >= nrows
+                                  and v is not None and v.numel() >= ncols)
+    _lib.check(getattr(_lib.load(), f"st_round_split_flat_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(s_next), _ptr(part), _ptr(v), nrows, ncols, row0,
+        col0, col1, eps, k, max_itr, semantics, span, _ptr(state),
+        _stream(mat.device)), "round_split_flat")
+
+
 def epilogue(s, v, state, eps: float, max_itr: int = _lib.ST_MAX_ITR,
              semantics: int = _lib.ST_SEM_SYCL) -> None:
     """Round epilogue: max, v *= s/m, stop test, λ = s[0], bookkeeping."""

@@ -111,6 +111,18 @@ class HipShardOps:
 
     def split_round(self, mat, s_cur, s_next, part, v, row0, col0, col1, eps, k, max_itr,
                     semantics, state, span):
+        # blocks where the flat round pays split it the same way
+        # (st_round_split_flat, its own partial-sum scratch instead of `part`)
+        nrows, ncols = mat.shape
+        if self.dev.flat_round_pays(nrows, ncols, mat.dtype):
+            key = ("split", nrows, ncols, col0, col1, mat.dtype)
+            if self._part is None or self._part[0] != key:
+                self._part = (key, self.dev.split_flat_scratch(nrows, ncols, col0, col1,
+                                                               mat.dtype, self.device))
+            self.dev.split_flat_round(mat, s_cur, s_next, self._part[1], v, state,
+                                      span=span, row0=row0, col0=col0, col1=col1, eps=eps,
+                                      k=k, max_itr=max_itr, semantics=semantics)
+            return
         self.dev.split_round(mat, s_cur, s_next, part, v, state, span=span, row0=row0,
                              col0=col0, col1=col1, eps=eps, k=k, max_itr=max_itr,
                              semantics=semantics)

@@ -329,6 +329,32 @@ int st_round_split_f64(double* d_mat, const double* d_s_cur,
                        unsigned int max_itr, unsigned int semantics, int span,
                        st_state* d_state, void* stream);
 
+/* The same two halves in the flat form (st_round_flat), for blocks where
+ * st_round_flat_pays: span 1 runs k_flat over the 4 KB column pieces that
+ * hold [col0, col1), span 2 over all pieces with the other columns (plus
+ * the m / stop / lambda / state work of k_flat's first row group), then
+ * sums remote-then-local partials into d_s_next and updates v.  d_part:
+ * scratch of st_round_split_flat_scratch(nrows, ncols, col0, col1)
+ * elements, shared by the two halves of a round.  A_{k+1}, v, m and stop
+ * are bit-identical to st_round_flat; s_{k+1} differs from it only in the
+ * summation order. */
+int st_round_split_flat_f32(float* d_mat, const float* d_s_cur,
+                            float* d_s_next, float* d_part, float* d_v,
+                            unsigned int nrows, unsigned int ncols,
+                            unsigned int row0, unsigned int col0,
+                            unsigned int col1, float eps, unsigned int k,
+                            unsigned int max_itr, unsigned int semantics,
+                            int span, st_state* d_state, void* stream);
+int st_round_split_flat_f64(double* d_mat, const double* d_s_cur,
+                            double* d_s_next, double* d_part, double* d_v,
+                            unsigned int nrows, unsigned int ncols,
+                            unsigned int row0, unsigned int col0,
+                            unsigned int col1, double eps, unsigned int k,
+                            unsigned int max_itr, unsigned int semantics,
+                            int span, st_state* d_state, void* stream);
+uint64_t st_round_split_flat_scratch(unsigned int nrows, unsigned int ncols,
+                                     unsigned int col0, unsigned int col1);
+
 /* Matrix-free round.  The transformed matrix of
  * round k is X^-1 A_0 X with x ∝ the product of all previous row-sum
  * vectors, so its row sums are (A_0 x) ⊘ x and A_0 never has to be

@@ -277,11 +277,71 @@ def test_split_round_matches_round(orc, dt, nrows, ncols, row0):
     assert np.array_equal(outs[2][1], base[1])           # local = all columns
 
 
-def test_sharded_overlap_single_gpu_bitwise(solver):
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("nrows,ncols,row0,col0,col1", [
+    (512, 1536, 512, 512, 1024), (1500, 1500, 0, 0, 1500), (1500, 1500, 0, 700, 700),
+    (7, 257, 100, 100, 107), (2049, 6000, 3000, 3000, 5049), (300, 3001, 5, 5, 305),
+    (64, 4096, 1024, 1000, 1030)])
+def test_split_flat_round_matches_flat(orc, dt, nrows, ncols, row0, col0, col1):
+    """st_round_split_flat_* local + remote == st_round_flat_*: A_{k+1}, v
+    and the state bit for bit; s_{k+1} to rounding (a piece straddling the
+    local range is summed in two parts), and bit for bit when the local
+    range is every column or empty."""
+    a = orc.random_matrix(ncols, 3, dt, nrows=nrows)
+    s_full = np.ascontiguousarray((orc.random_matrix(ncols, 9, dt, nrows=1)[0]
+                                   + dt(0.5)).astype(dt))
+    v0 = orc.random_matrix(ncols, 5, dt, nrows=1)[0]
+    outs = []
+    for split in (False, True):
+        ta, ts, tv = (torch.from_numpy(x).to(DEV) for x in (a, s_full, v0))
+        s_next = torch.empty(nrows, dtype=TD[dt], device=DEV)
+        state = dev.new_state(DEV)
+        if split:
+            part = dev.split_flat_scratch(nrows, ncols, col0, col1, TD[dt], DEV)
+            part.fill_(float("nan"))              # every slot read must be written
+            dev.split_flat_round(ta, ts, None, part, None, state, span=dev.SPAN_LOCAL,
+                                 row0=row0, col0=col0, col1=col1, eps=1e-3, k=3)
+            dev.split_flat_round(ta, ts, s_next, part, tv, state, span=dev.SPAN_REMOTE,
+                                 row0=row0, col0=col0, col1=col1, eps=1e-3, k=3)
+        else:
+            part = dev.flat_scratch(nrows, ncols, TD[dt], DEV)
+            dev.flat_round(ta, ts, s_next, part, tv, state, row0=row0, eps=1e-3, k=3)
+        outs.append((to_np(ta), to_np(s_next), to_np(tv), dev.read_state(state)))
+    (a0, s0, v0_, st0), (a1, s1, v1, st1) = outs
+    ref = orc.compute_next(a, s_full, row0=row0)
+    assert np.array_equal(a1, ref) and np.array_equal(a1, a0)
+    assert np.array_equal(v1, v0_) and st1 == st0
+    tol = 1e-14 if dt == np.float64 else 1e-6
+    assert np.max(np.abs(s1 - s0) / s0) <= tol
+    if col0 == col1 or (col0, col1) == (0, ncols):
+        assert np.array_equal(s1, s0)
+
+
+def test_split_flat_round_gating(orc):
+    """Both halves are no-ops once a previous round stopped."""
+    n = 700
+    a = torch.from_numpy(orc.random_matrix(n, 1)).to(DEV)
+    s = torch.full((n,), 4.0, dtype=torch.float64, device=DEV)     # constant: stops
+    s_next = torch.empty_like(s)
+    v = torch.ones_like(s)
+    part = dev.split_flat_scratch(n, n, 100, 300, torch.float64, DEV)
+    state = dev.new_state(DEV)
+    for span in (dev.SPAN_LOCAL, dev.SPAN_REMOTE):
+        dev.split_flat_round(a, s, s_next, part, v, state, span=span, col0=100, col1=300, k=0)
+    assert dev.read_state(state)["end"] == 1
+    keep, vkeep = a.clone(), v.clone()
+    for span in (dev.SPAN_LOCAL, dev.SPAN_REMOTE):
+        dev.split_flat_round(a, s * 3.0, s_next, part, v, state, span=span, col0=100,
+                             col1=300, k=1)
+    assert torch.equal(a, keep) and torch.equal(v, vkeep)
+
+
+@pytest.mark.parametrize("n", [3000, 9216])
+def test_sharded_overlap_single_gpu_bitwise(solver, n):
     """overlap=True at P = 1 (streams, events and the split launches; the
-    gather is empty) gives bitwise the one-launch result."""
+    gather is empty) gives bitwise the unsplit result: one-launch round at
+    3000, the flat round at 9216 (648 MiB)."""
     from eigen_value_amd.sharded import ShardedSimilarityTransform
-    n = 3000
     res = []
     for overlap in (False, True):
         sh = ShardedSimilarityTransform(n, torch.float64, overlap=overlap)
@@ -342,16 +402,18 @@ def test_sharded_two_ranks_on_one_gpu(tmp_path, solver, n):
         assert np.array_equal(np.load(tmp_path / f"v{r}.npy"), to_np(v))
 
 
-def test_sharded_overlap_two_ranks_on_one_gpu(tmp_path, solver):
+@pytest.mark.parametrize("n", [2502, 9216])
+def test_sharded_overlap_two_ranks_on_one_gpu(tmp_path, solver, n):
     """P = 2 with the overlapped exchange (communication stream, events,
     split launches; gloo on one GPU): same iterations and rounds as the
-    single-GPU solve, λ and v to fp64 rounding, identical on both ranks."""
+    single-GPU solve, λ and v to fp64 rounding, identical on both ranks.
+    2502: 1251 rows each on the grid-stride split; 9216: 324 MiB blocks on
+    the flat split."""
     import socket
     import torch.multiprocessing as mp
     with socket.socket() as sk:
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
-    n = 2502                                   # 1251 rows each (even split, odd size)
     mp.spawn(_gpu_gloo_worker, args=(2, port, n, str(tmp_path), True), nprocs=2, join=True)
     a = dev.generate("random", n, torch.float64, seed=6, device=DEV)
     lam, v, it, st = solver.solve(a)

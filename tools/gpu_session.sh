@@ -57,6 +57,7 @@ for s in $STEPS; do
     overlap) # the overlapped exchange: N = 1 (split launches, empty gather) and the rehearsal
       step bench_overlap_p1 600 python bench.py --overlap --no-cpu --no-north-star --no-headline
       step bench_overlap_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu --overlap --no-overlap-leg ;;
+    split) step split_cost 600 python3 tools/split_cost.py ;;
     fp32)  step fp32_study 600 python3 tools/fp32_study.py --out "$OUT/fp32_study.json" ;;
     profile)
       # one workload per profiled command, so every rocprofv3 summary row
