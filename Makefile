@@ -12,7 +12,7 @@ LIB      := eigen_value_amd/lib/libsimilarity_transform.so
 
 all: $(LIB) oracle
 
-build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h
+build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h eigen_value_amd/csrc/st_device.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -680,8 +680,45 @@ split_full_pieces(uint32_t ncols, uint32_t ppr, uint32_t col0, uint32_t col1,
   nfull = pb > pa ? pb - pa : 0u;
 }
 
+// How a flat workgroup learns that its launch follows the stopping round
+// (state->end != 0 && end <= k).  Millions of short workgroups each pay
+// this, so its latency matters (a persistent kernel pays it once per CU):
+//   kGateAtomic   agent-scope atomic load (an L2 round trip) before any
+//                 matrix load is issued
+//   kGatePlain    plain load, served from the CU's L1 after the first
+//                 workgroup of the launch on that CU.  Exact: `end` only
+//                 changes inside the stopping launch k (to k + 1, which
+//                 gates nothing in launch k), and every launch starts with
+//                 the L1 invalidated
+//   kGateNone     no gate (sweep ceiling only; not a valid solve)
+//   kGateSpec     the matrix loads are issued first and the atomic gate is
+//                 read while they are in flight; a gated launch then reads
+//                 but never writes
+// The plain load compiles to a scalar load (uniform address, nothing stored
+// before it); it times like no gate at all and 1.8 % faster than the atomic
+// gate per round at 32768^2 fp64, 3.5 % on the P = 8 row block, within
+// -0.7 % (8192^2 fp64) ... +3.5 % elsewhere
+// (profiles/r01_sweep_gate*.log, SWEEP_GATE=1 tools/sweep_dir), so the
+// library launches k_flat with it.
+enum { kGateAtomic = 0, kGatePlain = 1, kGateNone = 2, kGateSpec = 3 };
+
+template <int GATE>
+__device__ __forceinline__ bool
+flat_gated(const st_state* state, uint32_t k)
+{
+  uint32_t e;
+  if constexpr (GATE == kGateNone)
+    return false;
+  else if constexpr (GATE == kGatePlain)
+    e = state->end; // not volatile: volatile bypasses the L1 (sc0 sc1)
+  else
+    e = __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return e != 0 && e <= k;
+}
+
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          bool FS = false, bool ALT = false, int BLK = kBlock, int SPLIT = 0>
+          bool FS = false, bool ALT = false, int BLK = kBlock, int SPLIT = 0,
+          int GATE = kGatePlain>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -702,10 +739,8 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // R rows of one column piece per workgroup (the piece's column scales are
   // loaded once for the R rows); PW: one partial per wave instead of a
   // workgroup combine (no barrier before the workgroup retires)
-  {
-    const uint32_t e =
-      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e != 0 && e <= k)
+  if constexpr (GATE != kGateSpec) {
+    if (flat_gated<GATE>(state, k))
       return;
   }
   using V = typename vec<T, W>::type;
@@ -745,16 +780,23 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
     sr[j] = r0 + j < nrows ? s_cur[row0 + r0 + j] : (T)1;
   }
+  // the piece's column scales, issued with the matrix loads (the stats of
+  // the first row group read them too)
+  V sc;
+  if (in_cols)
+    sc = *reinterpret_cast<const V*>(s_cur + c);
+  if constexpr (GATE == kGateSpec) {
+    if (flat_gated<kGateAtomic>(state, k))
+      return;
+  }
   if constexpr (FS) {
     if (rg == 0) { // uniform per workgroup
       __shared__ T mx_sh[NW];
       T mx = (T)0;
       int ok = 1;
-      if (in_cols) {
-        const V sc0 = *reinterpret_cast<const V*>(s_cur + c);
-        stats_at<T, W>(s_cur, sc0, c / W, ncols, semantics == ST_SEM_SYCL, eps,
+      if (in_cols)
+        stats_at<T, W>(s_cur, sc, c / W, ncols, semantics == ST_SEM_SYCL, eps,
                        mx, ok);
-      }
       int fail = ok ? 0 : 1;
       mx = wave_max(mx);
       if ((threadIdx.x & 63) == 0)
@@ -770,7 +812,6 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     }
   }
   if (in) {
-    const V sc = *reinterpret_cast<const V*>(s_cur + c);
 #pragma unroll
     for (int j = 0; j < R; j++) {
       if (r0 + j < nrows) {

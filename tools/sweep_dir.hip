@@ -184,23 +184,26 @@ flat_seq(const Bufs<T>& b, T* part)
 
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
-template <typename T, int R, bool NT = true, bool ALT = false, int FB = 256>
+template <typename T, int R, bool NT = true, bool ALT = false, int FB = 256,
+          int GATE = kGateAtomic>
 static void
-flat2_seq(const Bufs<T>& b, T* part)
+flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
 {
+  // lds: dynamic LDS reserved per workgroup (limits workgroups per CU)
   constexpr int W = 16 / sizeof(T);
   const unsigned ppr = (b.n + FB * W - 1) / (FB * W);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   float flat = time_seq([&](int k) {
-    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB>),
-                       dim3(grid), dim3(FB), 0, 0, b.a, b.s, part, b.v, b.nr,
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB, 0, GATE>),
+                       dim3(grid), dim3(FB), lds, 0, b.a, b.s, part, b.v, b.nr,
                        b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
     hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
                        part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d  round (2 launches) %8.4f ms %7.1f GB/s\n",
-              R, (int)NT, (int)ALT, FB, flat, bytes / (flat * 1e-3) / 1e9);
+  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d gate=%d lds=%5u  round (2 launches) "
+              "%8.4f ms %7.1f GB/s\n",
+              R, (int)NT, (int)ALT, FB, GATE, lds, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
 template <typename T>
@@ -298,6 +301,62 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_OCC")) { // flat workgroups per CU (LDS-limited)
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (unsigned lds : { 0u, 18u << 10, 22u << 10, 26u << 10, 32u << 10, 40u << 10 }) {
+      if (big) {
+        flat2_seq<T, 2, true, true, 256, kGatePlain>(b, part, lds);
+        flat2_seq<T, 2, true, true, 256, kGateAtomic>(b, part, lds);
+      } else {
+        flat2_seq<T, 2, false, true, 256, kGatePlain>(b, part, lds);
+        flat2_seq<T, 2, false, true, 256, kGateAtomic>(b, part, lds);
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
+  if (std::getenv("SWEEP_GATE")) { // how the flat workgroups read the gate
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (int rep = 0; rep < 2; rep++) {
+      if (big) {
+        flat2_seq<T, 2, true, true, 256, kGateAtomic>(b, part);
+        flat2_seq<T, 2, true, true, 256, kGatePlain>(b, part);
+        flat2_seq<T, 2, true, true, 256, kGateSpec>(b, part);
+        flat2_seq<T, 2, true, true, 256, kGateNone>(b, part);
+        flat2_seq<T, 2, true, true, 64, kGatePlain>(b, part);
+        flat2_seq<T, 2, true, true, 64, kGateNone>(b, part);
+        flat2_seq<T, 4, true, true, 64, kGatePlain>(b, part);
+      } else {
+        flat2_seq<T, 2, false, true, 256, kGateAtomic>(b, part);
+        flat2_seq<T, 2, false, true, 256, kGatePlain>(b, part);
+        flat2_seq<T, 2, false, true, 256, kGateSpec>(b, part);
+        flat2_seq<T, 2, false, true, 256, kGateNone>(b, part);
+        flat2_seq<T, 2, false, true, 64, kGatePlain>(b, part);
+        flat2_seq<T, 2, false, true, 64, kGateNone>(b, part);
+        flat2_seq<T, 4, false, true, 64, kGatePlain>(b, part);
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_FLAT")) { // the flat round vs k_round
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
