@@ -716,8 +716,25 @@ flat_gated(const st_state* state, uint32_t k)
   return e != 0 && e <= k;
 }
 
+// The piece order of an odd round (ALT): 1 = the grid reversed; 2 = the
+// grid reversed in steps of 8 workgroups with each workgroup's position in
+// its step kept, so that (workgroups going to XCD blockIdx % 8) every piece
+// is handled by the same XCD - and the same L2 - in every round.  The last
+// gridDim % 8 workgroups keep their place.
+template <int ALT>
+__device__ __forceinline__ uint32_t
+flat_reverse(uint32_t b, uint32_t g)
+{
+  if constexpr (ALT == 1) {
+    return g - 1 - b;
+  } else {
+    const uint32_t g8 = g & ~7u;
+    return b < g8 ? g8 - 8 - (b & ~7u) + (b & 7u) : b;
+  }
+}
+
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          bool FS = false, bool ALT = false, int BLK = kBlock, int SPLIT = 0,
+          bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
@@ -746,7 +763,8 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
   __shared__ T red[NW][R];
-  const uint32_t b = (ALT && (k & 1u)) ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+  const uint32_t b = (ALT != 0 && (k & 1u)) ? flat_reverse<ALT>(blockIdx.x, gridDim.x)
+                                            : blockIdx.x;
   uint32_t rg, p;                                  // p: index into this row's parts
   if constexpr (SPLIT == 2) {
     // the pieces wholly inside [col0, col1) have nothing to do past row

@@ -54,7 +54,7 @@ check_launch(const char* what)
 //     <= 12288 columns cached), 2 above; one workgroup per CU; 2 rows and
 //     2 (<= 128 MiB) or 4 (<= 32 MiB) workgroups per CU on small matrices;
 //     1 row per group below 1024 rows.  (The solve loops hand blocks of
-//     288 MiB and more to the flat round below; st_round_* keeps these
+//     144 MiB and more to the flat round below; st_round_* keeps these
 //     shapes at every size.)
 //   * k_mfree: 4 rows per group, 2 workgroups per CU (2 rows between 64
 //     and 512 MiB).
@@ -104,14 +104,19 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   return { 4, true, 512u };
 }
 
-// the flat round (k_flat + k_parts) for blocks of >= 288 MiB, with cached
+// the flat round (k_flat + k_parts) for blocks of >= 144 MiB, with cached
 // accesses and alternating piece order below 2 GiB (the memory-side cache
-// then serves the start of each round) and non-temporal ones above:
-// tools/sweep_dir.hip SWEEP_FLAT=1, profiles/r01_sweep_flat_cached.log
-// (32768^2 fp64 2.72 ms vs 3.06 for k_round; 16384^2 0.68 vs 0.76; 8192^2
-// 0.163 vs 0.168; the 2880x23040 block 0.168 vs 0.184; at 256 MiB and
-// below k_round stays ahead)
+// then serves the start of each round; odd rounds reverse the pieces in
+// steps of 8 workgroups so that every piece stays on its XCD and L2,
+// flat_reverse<2>) and non-temporal ones above:
+// tools/sweep_dir.hip SWEEP_FLAT=1 / SWEEP_XCD=1,
+// profiles/r01_sweep_flat_cached.log, r01_sweep_xcd{,_round}.log
+// (32768^2 fp64 2.68 ms vs 3.06 for k_round; 16384^2 0.67 vs 0.76; 8192^2
+// fp64 0.160 vs 0.168, fp32 0.079 vs 0.080; the 2880x23040 block 0.165 vs
+// 0.182; 6144^2 fp32 (144 MiB) 0.0472 vs 0.0478; at 128 MiB and below
+// k_round stays ahead: 4096^2 fp64 0.0412 vs 0.0426)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
+constexpr int kFlatAlt = 2;  // odd rounds: pieces reversed per XCD (flat_reverse)
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
 // than in a k_stats launch of their own (three)
 constexpr bool kFlatFusedStats = true;
@@ -119,7 +124,7 @@ constexpr bool kFlatFusedStats = true;
 inline bool
 flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  return block_bytes(nrows, ncols, elem) >= ((size_t)288 << 20);
+  return block_bytes(nrows, ncols, elem) >= ((size_t)144 << 20);
 }
 
 inline bool
@@ -462,7 +467,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, true>), dim3(grid),
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt>), dim3(grid),
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
       st, eps, max_itr, semantics);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
@@ -473,7 +478,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, true>),
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt>),
       dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols,
       ppr, row0, k, st, eps, max_itr, semantics);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
@@ -568,13 +573,13 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
     // about to re-read (profiles/r01_split_cost.log)
     if (NT || col1 - col0 < ncols)
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, true, kBlock, 1>),
+        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
         dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
         nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
         col1);
     else
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, true, kBlock, 1>),
+        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
         dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
         nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
         col1);
@@ -585,7 +590,7 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
   uint32_t pa, nfull;
   dev::split_full_pieces<PW>(ncols, ppr, col0, col1, pa, nfull);
   hipLaunchKernelGGL(
-    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, true, kBlock, 2>),
+    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 2>),
     dim3(ppr + (ngroups - 1) * (ppr - nfull)), dim3(kBlock), 0, stream, a,
     s_cur, part, v, nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
     0u, col0, col1);

@@ -184,7 +184,7 @@ flat_seq(const Bufs<T>& b, T* part)
 
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
-template <typename T, int R, bool NT = true, bool ALT = false, int FB = 256,
+template <typename T, int R, bool NT = true, int ALT = 0, int FB = 256,
           int GATE = kGateAtomic>
 static void
 flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
@@ -204,6 +204,51 @@ flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
   std::printf("  flat2 r=%d nt=%d alt=%d blk=%d gate=%d lds=%5u  round (2 launches) "
               "%8.4f ms %7.1f GB/s\n",
               R, (int)NT, (int)ALT, FB, GATE, lds, flat, bytes / (flat * 1e-3) / 1e9);
+}
+
+// k_round with the library's launch shape (round_shape in st_kernels.hip)
+template <typename T, int ROWS, int NT>
+static float
+round_shape_seq(const Bufs<T>& b, unsigned cap)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ng = b.nr / ROWS;
+  const unsigned grid = cap < ng ? cap : ng;
+  return time_seq([&](int k) {
+    hipLaunchKernelGGL((k_round<T, ROWS, W, 2, 0, NT, 256, true>), dim3(grid),
+                       dim3(256), 0, 0, b.a, b.s, b.sn, b.v, ng, 0u, b.n, 0u,
+                       (T)0, (uint32_t)k, 1u << 30, 0u, b.st);
+  });
+}
+
+template <typename T>
+static void
+round_lib(const Bufs<T>& b)
+{
+  const size_t by = (size_t)b.nr * b.n * sizeof(T);
+  float t;
+  int rows;
+  if (b.nr < 1024) {
+    rows = 1;
+    t = round_shape_seq<T, 1, kCached>(b, 512);
+  } else if (by <= ((size_t)32 << 20)) {
+    rows = 2;
+    t = round_shape_seq<T, 2, kCached>(b, 1024);
+  } else if (by < ((size_t)128 << 20)) {
+    rows = 2;
+    t = round_shape_seq<T, 2, kCached>(b, 512);
+  } else if (by < ((size_t)1 << 30)) {
+    rows = b.n <= 12288 ? 4 : 2;
+    t = rows == 4 ? round_shape_seq<T, 4, kCached>(b, 256)
+                  : round_shape_seq<T, 2, kCached>(b, 256);
+  } else {
+    rows = (size_t)b.n * sizeof(T) <= ((size_t)96 << 10) ? 4 : 2;
+    t = rows == 4 ? round_shape_seq<T, 4, kNtBoth>(b, 256)
+                  : round_shape_seq<T, 2, kNtBoth>(b, 256);
+  }
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
+  std::printf("  k_round (library shape, rows=%d)  %8.4f ms %7.1f GB/s\n", rows, t,
+              bytes / (t * 1e-3) / 1e9);
 }
 
 template <typename T>
@@ -301,6 +346,32 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_XCD")) { // odd-round piece order: global vs per-XCD reversal
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (int rep = 0; rep < 2; rep++) {
+      if (std::getenv("SWEEP_XCD_ROUND"))
+        round_lib<T>(b);
+      if (big) {
+        flat2_seq<T, 2, true, 1, 256, kGatePlain>(b, part);
+        flat2_seq<T, 2, true, 2, 256, kGatePlain>(b, part);
+        flat2_seq<T, 2, true, 0, 256, kGatePlain>(b, part);
+      }
+      flat2_seq<T, 2, false, 1, 256, kGatePlain>(b, part);
+      flat2_seq<T, 2, false, 2, 256, kGatePlain>(b, part);
+      flat2_seq<T, 2, false, 0, 256, kGatePlain>(b, part);
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_OCC")) { // flat workgroups per CU (LDS-limited)
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
