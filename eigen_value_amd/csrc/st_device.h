@@ -66,15 +66,83 @@ hsum(const typename vec<T, W>::type& y)
   }
 }
 
-// fixed tree over the 64 lanes; lane 0 holds the result
+// DPP lane move (gfx9 data-parallel primitives; 64-bit values move as two
+// dwords).  Lanes outside ROW_MASK read 0.
+template <int CTRL, int ROW_MASK = 0xf, typename T>
+__device__ __forceinline__ T
+dpp_mov(T x)
+{
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(
+      0, __float_as_int((float)x), CTRL, ROW_MASK, 0xf, false));
+  } else {
+    const long long b = __double_as_longlong((double)x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf,
+                                               false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL,
+                                               ROW_MASK, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ T
+read_lane63(T x)
+{
+  if constexpr (sizeof(T) == 4) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int((float)x), 63));
+  } else {
+    const long long b = __double_as_longlong((double)x);
+    const int lo = __builtin_amdgcn_readlane((int)b, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), 63);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+  }
+}
+
+// Sum over the 64 lanes in a fixed tree, returned in every lane: pairs and
+// quads (quad_perm), the four quads of each row of 16 (row_ror 4, 8), then
+// the rows (row_bcast 15 into rows 1 and 3, row_bcast 31 into rows 2 and
+// 3); lane 63 ends with ((R3 + R2) + (R1 + R0)) and is broadcast.  All DPP
+// (VALU) - no LDS permutes - and the same order in every kernel, so a row
+// sum never depends on which kernel or partition computed it.
 template <typename T>
 __device__ __forceinline__ T
 wave_sum(T x)
 {
+  x += dpp_mov<0xB1>(x);       // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);       // quad_perm [2,3,0,1]
+  x += dpp_mov<0x124>(x);      // row_ror 4
+  x += dpp_mov<0x128>(x);      // row_ror 8
+  x += dpp_mov<0x142, 0xa>(x); // row_bcast 15
+  x += dpp_mov<0x143, 0xc>(x); // row_bcast 31
+  return read_lane63(x);
+}
+
+// wave_sum of NR independent values, step by step across them (no stall
+// between the dependent DPP steps of one value); the sums are left in lane
+// 63 (bitwise wave_sum's results)
+template <typename T, int NR>
+__device__ __forceinline__ void
+wave_sum_rows(T (&x)[NR])
+{
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-    x += __shfl_down(x, off, 64);
-  return x;
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0xB1>(x[i]);
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0x4E>(x[i]);
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0x124>(x[i]);
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0x128>(x[i]);
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0x142, 0xa>(x[i]);
+#pragma unroll
+  for (int i = 0; i < NR; i++)
+    x[i] += dpp_mov<0x143, 0xc>(x[i]);
 }
 
 template <typename T>
@@ -1241,6 +1309,157 @@ k_fill(T* __restrict__ x, uint64_t count, T value)
   for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < count;
        i += (uint64_t)gridDim.x * kBlock)
     x[i] = value;
+}
+
+// ---------------------------------------------------------------------------
+// the whole solve in ONE workgroup, for matrices that fit its registers
+// (N <= 64*W: 128 fp64, 256 fp32; N % W == 0)
+//
+// A small solve is launch-bound: ~10 rounds of a few microseconds of work,
+// each a launch plus the host's batch checks.  Here 16 waves keep the
+// matrix in VGPRs for the whole iteration (row r on wave r % 16, lane l
+// holding its 16-byte chunk l; at most 16 fp64 or 64 fp32 values per lane),
+// s and v in LDS, and run every round back to back with workgroup barriers
+// only.  Each round computes exactly what k_round computes, bit for bit:
+//   row sums   hsum of the lane's chunk, then wave_sum over the 64 lanes
+//              (k_round / k_fused: a single chunk per lane at these sizes,
+//              the other waves' zeros add nothing)
+//   m_k, stop  max from 0 and the (cyclic) pair test over s_k
+//   v          v[r] * (s_k[r] / m_k)
+//   transform  x * ((1/s_r) * s_c)  (or ((1/s_r) * x) * s_c, main.py)
+// and, like k_round, the stopping (or last) round still transforms and
+// sums, so the final matrix equals the per-round loop's.  The matrix, v and
+// the state are written back at the end; s_k is not.
+// ---------------------------------------------------------------------------
+constexpr int kSmallBlock = 1024; // 16 waves
+constexpr int kSmallWaves = kSmallBlock / 64;
+
+template <typename T>
+constexpr uint32_t
+small_solve_max_n()
+{
+  return 64u * (16u / sizeof(T));
+}
+
+template <typename T, int ORDER, int RPW>
+__global__ __launch_bounds__(kSmallBlock) void
+k_solve_small(T* a, T* __restrict__ v_out, uint32_t n, T eps, uint32_t max_itr,
+              uint32_t semantics, st_state* state)
+{
+  // RPW: rows per wave, the power of two >= ceil(n / 16) (the launcher
+  // picks the instantiation; rows r = wave + 16 i past n are zeros)
+  constexpr int W = 16 / sizeof(T);
+  constexpr uint32_t NMAX = small_solve_max_n<T>();
+  static_assert(RPW * kSmallWaves <= (int)NMAX, "rows per wave");
+  using V = typename vec<T, W>::type;
+  __shared__ V s_sh[2][NMAX / W];
+  __shared__ T v_sh[NMAX];
+  __shared__ T inv_sh[NMAX]; // 1 / s_k[r], once per row instead of per lane
+  __shared__ T mx_sh[kSmallWaves];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint32_t nv = n / W; // chunks per row
+  const bool has = lane < nv;
+  const bool cyclic = semantics == ST_SEM_SYCL;
+  T* s0 = reinterpret_cast<T*>(s_sh[0]);
+  T* s1 = reinterpret_cast<T*>(s_sh[1]);
+
+  V x[RPW];
+  T t[RPW];
+#pragma unroll
+  for (int i = 0; i < RPW; i++) {
+    const uint32_t r = wave + kSmallWaves * i;
+    if (has && r < n)
+      x[i] = *reinterpret_cast<const V*>(a + (size_t)r * n + lane * W);
+    else
+      x[i] = (V)(T)0;
+  }
+  // K0: s_0 = rowsum(A_0)
+#pragma unroll
+  for (int i = 0; i < RPW; i++)
+    t[i] = has ? hsum<T, W>(x[i]) : (T)0;
+  wave_sum_rows<T, RPW>(t);
+  if (lane == 63) {
+#pragma unroll
+    for (int i = 0; i < RPW; i++)
+      if (wave + kSmallWaves * i < n)
+        s0[wave + kSmallWaves * i] = t[i];
+  }
+  if (threadIdx.x < n)
+    v_sh[threadIdx.x] = (T)1; // initialise_eigen_vector (cpp:34)
+
+  T* sc_ = s0;
+  T* sn_ = s1;
+  uint32_t k = 0;
+  for (;; k++) {
+    __syncthreads(); // s_k complete
+    // m_k and stop_k (find_max starts from 0, cpp:185; cpp:413-421)
+    T mx = (T)0;
+    int ok = 1;
+    if (threadIdx.x < n) {
+      const T e0 = sc_[threadIdx.x];
+      inv_sh[threadIdx.x] = (T)1 / e0;
+      mx = e0 > mx ? e0 : mx;
+      const uint32_t nx = threadIdx.x + 1;
+      if (nx < n || cyclic) {
+        const T d = e0 - sc_[nx < n ? nx : 0];
+        ok = (d < (T)0 ? -d : d) < eps ? 1 : 0;
+      }
+    }
+    mx = wave_max(mx);
+    if (lane == 0)
+      mx_sh[wave] = mx;
+    const int stop = __syncthreads_and(ok);
+    T m = mx_sh[0];
+#pragma unroll
+    for (int w = 1; w < kSmallWaves; w++)
+      m = mx_sh[w] > m ? mx_sh[w] : m;
+    if (threadIdx.x < n) // cpp:260
+      v_sh[threadIdx.x] = v_sh[threadIdx.x] * (sc_[threadIdx.x] / m);
+    const bool last = stop || k + 1 >= max_itr;
+    if (last && threadIdx.x == 0) {
+      state->lambda = (double)sc_[0]; // cpp:60-65
+      state->max = (double)m;
+      state->stop = stop ? 1u : 0u;
+      state->round = k;
+      state->iters = stop ? (semantics == ST_SEM_SYCL ? k : k + 1) : max_itr;
+      state->end = k + 1;
+      state->done = 1u;
+    }
+    // A_{k+1} = D_k^-1 A_k D_k and s_{k+1} (as k_round, also in the last round)
+    const V sc = has ? reinterpret_cast<const V*>(sc_)[lane] : (V)(T)1;
+#pragma unroll
+    for (int i = 0; i < RPW; i++) {
+      const uint32_t r = wave + kSmallWaves * i;
+      const T inv = r < n ? inv_sh[r] : (T)1;
+      if constexpr (ORDER == 0)
+        x[i] = x[i] * (inv * sc); // cpp:324-325
+      else
+        x[i] = (inv * x[i]) * sc; // main.py:13-16
+      t[i] = has ? hsum<T, W>(x[i]) : (T)0;
+    }
+    wave_sum_rows<T, RPW>(t);
+    if (lane == 63) {
+#pragma unroll
+      for (int i = 0; i < RPW; i++)
+        if (wave + kSmallWaves * i < n)
+          sn_[wave + kSmallWaves * i] = t[i];
+    }
+    T* tmp = sc_;
+    sc_ = sn_;
+    sn_ = tmp;
+    if (last)
+      break;
+  }
+  // write back: the transformed matrix and v
+#pragma unroll
+  for (int i = 0; i < RPW; i++) {
+    const uint32_t r = wave + kSmallWaves * i;
+    if (has && r < n)
+      *reinterpret_cast<V*>(a + (size_t)r * n + lane * W) = x[i];
+  }
+  __syncthreads();
+  if (threadIdx.x < n)
+    v_out[threadIdx.x] = v_sh[threadIdx.x];
 }
 
 } // namespace dev

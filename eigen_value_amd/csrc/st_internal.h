@@ -63,5 +63,12 @@ int launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
                     uint32_t semantics, st_state* st, hipStream_t stream);
 template <typename T>
 int launch_fill(T* x, uint64_t count, T value, hipStream_t stream);
+// the whole solve in one workgroup (k_solve_small): v = 1, s_0, every round,
+// the final state; for n <= 128 (fp64) / 256 (fp32), n % (16/sizeof(T)) == 0
+template <typename T>
+bool solve_small_fits(const T* a, uint32_t n);
+template <typename T>
+int launch_solve_small(T* a, T* v, uint32_t n, T eps, uint32_t max_itr,
+                       uint32_t semantics, st_state* st, hipStream_t stream);
 
 } // namespace st

@@ -750,6 +750,63 @@ launch_generate(T* a, uint32_t nrows, uint32_t ncols, uint32_t row0,
   return check_launch("generate");
 }
 
+template <typename T>
+bool
+solve_small_fits(const T* a, uint32_t n)
+{
+  constexpr uint32_t W = 16 / sizeof(T);
+  return n > 0 && n <= dev::small_solve_max_n<T>() && n % W == 0 &&
+         aligned16(a);
+}
+
+template <typename T>
+int
+launch_solve_small(T* a, T* v, uint32_t n, T eps, uint32_t max_itr,
+                   uint32_t semantics, st_state* st, hipStream_t stream)
+{
+  ST_REQUIRE(a && v && st, "solve_small: null pointer");
+  ST_REQUIRE(solve_small_fits<T>(a, n),
+             "solve_small: n = %u does not fit one workgroup", n);
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "solve_small: bad semantics %u",
+             semantics);
+  ST_REQUIRE(max_itr > 0, "solve_small: max_itr must be > 0");
+  // rows per wave: the power of two >= ceil(n / 16)
+  const uint32_t rows = (n + dev::kSmallWaves - 1) / dev::kSmallWaves;
+  auto go = [&](auto order, auto rpw) {
+    hipLaunchKernelGGL(
+      (dev::k_solve_small<T, decltype(order)::value, decltype(rpw)::value>),
+      dim3(1), dim3(dev::kSmallBlock), 0, stream, a, v, n, eps, max_itr,
+      semantics, st);
+  };
+  auto by_rows = [&](auto order) {
+    if (rows <= 1)
+      go(order, std::integral_constant<int, 1>{});
+    else if (rows <= 2)
+      go(order, std::integral_constant<int, 2>{});
+    else if (rows <= 4)
+      go(order, std::integral_constant<int, 4>{});
+    else if constexpr (sizeof(T) == 8)
+      go(order, std::integral_constant<int, 8>{});
+    else if (rows <= 8)
+      go(order, std::integral_constant<int, 8>{});
+    else
+      go(order, std::integral_constant<int, 16>{});
+  };
+  if (semantics == ST_SEM_MAINPY)
+    by_rows(std::integral_constant<int, 1>{});
+  else
+    by_rows(std::integral_constant<int, 0>{});
+  return check_launch("solve_small");
+}
+
+template bool solve_small_fits<float>(const float*, uint32_t);
+template bool solve_small_fits<double>(const double*, uint32_t);
+template int launch_solve_small<float>(float*, float*, uint32_t, float,
+                                       uint32_t, uint32_t, st_state*,
+                                       hipStream_t);
+template int launch_solve_small<double>(double*, double*, uint32_t, double,
+                                        uint32_t, uint32_t, st_state*,
+                                        hipStream_t);
 template int launch_rowsum<float>(const float*, float*, uint32_t, uint32_t,
                                   hipStream_t);
 template int launch_rowsum<double>(const double*, double*, uint32_t, uint32_t,

@@ -229,17 +229,22 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   };
   int rc = 0;
 
+  // a matrix that fits one workgroup's registers runs the whole solve in a
+  // single launch, bit-identical to the round loop below; per-round timing
+  // and ST_FLAG_ROUND_LOOP keep the loop
+  const bool single = !mfree && !timed && (o.flags & ST_FLAG_ROUND_LOOP) == 0 &&
+                      solve_small_fits<T>(d_mat, n);
   const auto t0 = std::chrono::steady_clock::now();
   ST_CHECK(hipMemsetAsync(c->d_state, 0, sizeof(st_state), s));
-  if (launch_fill<T>(d_v, n, (T)1, s)) // initialise_eigen_vector, cpp:34
+  if (!single && launch_fill<T>(d_v, n, (T)1, s)) // initialise_eigen_vector, cpp:34
     return -1;
-  if (timed) {
+  if (timed) { // (never single: k_solve_small does v = 1 and s_0 itself)
     ev.resize(2, nullptr);
     if (mk(&ev[0]) || mk(&ev[1]))
       return -1;
     (void)hipEventRecord(ev[0], s);
   }
-  if (launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) // K0
+  if (!single && launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) // K0
     return -1;
   if (timed)
     (void)hipEventRecord(ev[1], s);
@@ -247,6 +252,12 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   const T eps = (T)o.eps;
   uint32_t enqueued = 0, cur = 0, batch_no = 0;
   bool done = false;
+  if (single) { // the whole loop in one launch (k_solve_small)
+    if (launch_solve_small<T>(d_mat, d_v, n, eps, o.max_itr, o.semantics,
+                              c->d_state, s))
+      return -1;
+    done = true;
+  }
   while (!done && enqueued < o.max_itr) {
     const uint32_t b = (o.max_itr - enqueued) < o.batch ? (o.max_itr - enqueued)
                                                         : o.batch;

@@ -266,8 +266,13 @@ class DeviceSolver:
 
     def solve(self, mat, *, inplace: bool = False, eps: Optional[float] = None,
               max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL, batch: int = 0,
-              time_kernels: bool = False, matrix_free: bool = False):
+              time_kernels: bool = False, matrix_free: bool = False,
+              round_loop: bool = False):
         """Returns (λ: float, v: tensor, iterations: int, stats: dict).
+
+        Matrices of n <= 128 (fp64) / 256 (fp32) run the whole solve in one
+        workgroup launch (bit-identical); ``round_loop`` forces one launch per
+        round instead (``ST_FLAG_ROUND_LOOP``).
 
         ``mat`` is transformed in place when ``inplace`` (it is the private
         working copy the reference makes, similarity_transform.cpp:14,19).
@@ -291,7 +296,8 @@ class DeviceSolver:
         ev = (ctypes.c_double if mat.dtype == torch.float64 else ctypes.c_float)()
         it = ctypes.c_uint32()
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
-                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0))
+                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
+                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()

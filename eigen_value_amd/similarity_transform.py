@@ -75,8 +75,10 @@ class EigenValue:
     def similarity_transform_ex(self, mat: np.ndarray, *, eps: Optional[float] = None,
                                 max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL,
                                 batch: int = 0, time_kernels: bool = False,
-                                matrix_free: bool = False):
+                                matrix_free: bool = False, round_loop: bool = False):
         """Extended call: options + statistics (``max_eigen_value_ex``).
+        ``round_loop`` keeps one launch per round where the whole solve would
+        fit one workgroup (``ST_FLAG_ROUND_LOOP``; identical results).
 
         Returns ``(λ, v, ts_ms, iterations, stats_dict)``."""
         m, n = mat.shape
@@ -85,7 +87,8 @@ class EigenValue:
         if mat.dtype not in (np.float32, np.float64):
             raise TypeError("float32 or float64 matrix required")
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
-                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0))
+                 | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
+                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()

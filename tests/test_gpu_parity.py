@@ -935,3 +935,61 @@ def test_cpp_kernel_tests():
     print(out.stdout)
     assert out.returncode == 0, out.stdout + out.stderr
     assert "similarity transform worked" in out.stdout
+
+
+# ---------------------------------------------------------------------------
+# the whole solve in one workgroup (k_solve_small, n <= 128 fp64 / 256 fp32)
+# against the per-round launch loop: bit-identical λ, v, iteration count and
+# final matrix
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dt,n", [(np.float64, 2), (np.float64, 8), (np.float64, 62),
+                                  (np.float64, 100), (np.float64, 128),
+                                  (np.float32, 4), (np.float32, 128), (np.float32, 252),
+                                  (np.float32, 256)])
+@pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
+@pytest.mark.parametrize("kind", ["hilbert", "random"])
+def test_single_launch_solve_matches_round_loop(solver, orc, dt, n, sem, kind):
+    mat = orc.hilbert(n, dt) if kind == "hilbert" else orc.random_matrix(n, 5, dt)
+    a1 = torch.from_numpy(mat).to(DEV)
+    a2 = a1.clone()
+    r1 = solver.solve(a1, inplace=True, semantics=sem)
+    r2 = solver.solve(a2, inplace=True, semantics=sem, round_loop=True)
+    assert r1[2] == r2[2] and r1[3]["rounds"] == r2[3]["rounds"]
+    assert r1[0] == r2[0]                                   # λ bitwise
+    assert torch.equal(r1[1], r2[1])                        # v bitwise
+    assert torch.equal(a1, a2)                              # final matrix bitwise
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL if sem == _lib.ST_SEM_SYCL
+                                   else orc.SEM_MAINPY)
+    assert r1[2] == ref.iter_count
+    tol = 1e-10 if dt == np.float64 else 1e-5
+    assert abs(r1[0] - ref.eigen_val) <= tol * ref.eigen_val
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
+def test_single_launch_exhaustion_and_eps(solver, orc, dt):
+    mat = orc.random_matrix(64, 9, dt)
+    for kw in (dict(eps=0.0, max_itr=5), dict(eps=1e-6), dict(max_itr=1)):
+        a1 = torch.from_numpy(mat).to(DEV)
+        a2 = a1.clone()
+        r1 = solver.solve(a1, inplace=True, **kw)
+        r2 = solver.solve(a2, inplace=True, round_loop=True, **kw)
+        assert (r1[0], r1[2], r1[3]["rounds"], r1[3]["converged"]) == \
+               (r2[0], r2[2], r2[3]["rounds"], r2[3]["converged"]), kw
+        assert torch.equal(r1[1], r2[1]) and torch.equal(a1, a2), kw
+    r = solver.solve(torch.from_numpy(mat).to(DEV), eps=0.0, max_itr=5)
+    assert r[2] == 5 and r[3]["rounds"] == 5 and r[3]["converged"] == 0
+
+
+def test_single_launch_dropin_is_one_launch(eigen, orc):
+    # the drop-in call at configs[0]'s size: Hilbert 128 fp32 (README.md:70,
+    # 9 rounds) — the single launch and the loop agree, and the single launch
+    # finishes the loop in less time than the per-round form
+    h = orc.hilbert(128, np.float32)
+    lam, v, ts, itr, st = eigen.similarity_transform_ex(h)
+    lam2, v2, ts2, itr2, st2 = eigen.similarity_transform_ex(h, round_loop=True)
+    assert itr == itr2 == 9 and lam == lam2 and np.array_equal(v, v2)
+    best = min(eigen.similarity_transform_ex(h)[4]["loop_ms"] for _ in range(5))
+    best_loop = min(eigen.similarity_transform_ex(h, round_loop=True)[4]["loop_ms"]
+                    for _ in range(5))
+    print(f"hilbert128 f32 loop_ms: single launch {best:.4f}, per round {best_loop:.4f}")
+    assert best < best_loop

@@ -346,6 +346,28 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_RB")) { // flat rows per workgroup x workgroup size (plain gate)
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+#define RB(R, FB)                                                              \
+  (big ? flat2_seq<T, R, true, 2, FB, kGatePlain>(b, part)                     \
+       : flat2_seq<T, R, false, 2, FB, kGatePlain>(b, part))
+    RB(1, 256); RB(2, 256); RB(4, 256);
+    RB(1, 128); RB(2, 128); RB(4, 128);
+    RB(1, 64);  RB(2, 64);  RB(4, 64);
+    RB(1, 512); RB(2, 512);
+#undef RB
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_XCD")) { // odd-round piece order: global vs per-XCD reversal
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
