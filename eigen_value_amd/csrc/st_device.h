@@ -941,6 +941,37 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
 }
 
+// k_parts with one THREAD per row (sweep variant): the row's partials in
+// four interleaved running sums, ((a0 + a1) + (a2 + a3)), no wave reduction
+template <typename T, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_parts_t(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
+          uint32_t ppr, uint32_t k, const st_state* state,
+          const T* __restrict__ s_cur = nullptr, T* __restrict__ v = nullptr,
+          uint32_t row0 = 0)
+{
+  if (flat_gated<kGatePlain>(state, k))
+    return;
+  const uint32_t r = blockIdx.x * BLK + threadIdx.x;
+  if (r >= nrows)
+    return;
+  const T* row = part + (size_t)r * ppr;
+  T a[4] = { (T)0, (T)0, (T)0, (T)0 };
+  uint32_t p = 0;
+  for (; p + 4 <= ppr; p += 4) {
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+      a[j] += row[p + j];
+  }
+  for (int j = 0; p < ppr; p++, j++)
+    a[j] += row[p];
+  s_next[r] = (a[0] + a[1]) + (a[2] + a[3]);
+  if (v != nullptr) {
+    const T m = (T)state->max;
+    v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
+  }
+}
+
 template <typename T, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,

@@ -185,11 +185,12 @@ flat_seq(const Bufs<T>& b, T* part)
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
 template <typename T, int R, bool NT = true, int ALT = 0, int FB = 256,
-          int GATE = kGateAtomic>
+          int GATE = kGateAtomic, int PT = 0>
 static void
 flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
 {
   // lds: dynamic LDS reserved per workgroup (limits workgroups per CU)
+  // PT: k_parts with one wave (0) or one thread (1) per row
   constexpr int W = 16 / sizeof(T);
   const unsigned ppr = (b.n + FB * W - 1) / (FB * W);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
@@ -197,13 +198,18 @@ flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
     hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB, 0, GATE>),
                        dim3(grid), dim3(FB), lds, 0, b.a, b.s, part, b.v, b.nr,
                        b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
-    hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
-                       part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
+    if constexpr (PT == 0)
+      hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
+                         part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v, 0u);
+    else
+      hipLaunchKernelGGL((k_parts_t<T>), dim3((b.nr + 255) / 256), dim3(256), 0,
+                         0, part, b.sn, b.nr, ppr, (uint32_t)k, b.st, b.s, b.v,
+                         0u);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d gate=%d lds=%5u  round (2 launches) "
+  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d gate=%d lds=%5u pt=%d  round (2 launches) "
               "%8.4f ms %7.1f GB/s\n",
-              R, (int)NT, (int)ALT, FB, GATE, lds, flat, bytes / (flat * 1e-3) / 1e9);
+              R, (int)NT, (int)ALT, FB, GATE, lds, PT, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
 // k_round with the library's launch shape (round_shape in st_kernels.hip)
@@ -346,6 +352,29 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_PARTS")) { // k_parts: one wave vs one thread per row
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (int rep = 0; rep < 3; rep++) {
+      if (big) {
+        flat2_seq<T, 2, true, 2, 256, kGatePlain, 0>(b, part);
+        flat2_seq<T, 2, true, 2, 256, kGatePlain, 1>(b, part);
+      } else {
+        flat2_seq<T, 2, false, 2, 256, kGatePlain, 0>(b, part);
+        flat2_seq<T, 2, false, 2, 256, kGatePlain, 1>(b, part);
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_RB")) { // flat rows per workgroup x workgroup size (plain gate)
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
