@@ -380,6 +380,23 @@ def main():
             "published_ms": {"Xeon Platinum 8358": 126, "i9-10920X": 510, "Xeon Gold 6128": 339,
                              "Xeon E5-2686 v4": 3759, "Iris Xe MAX": 2509, "UHD P630": 8259},
             "speedup_vs_fastest_published": round(126.0 / (st32["h2d_ms"] + st32["loop_ms"]), 1)}
+        # configs[0]'s size (128x128 Hilbert) on the GPU through the same
+        # drop-in call: the whole solve is ONE workgroup launch
+        # (k_solve_small); the per-round launch loop beside it
+        c0 = {}
+        with EigenValue() as e:
+            for name, dt in (("f32", np.float32), ("f64", np.float64)):
+                h = (dt(1.0) / (np.arange(128)[:, None] + np.arange(128)[None, :] + 1)
+                     .astype(dt))
+                e.similarity_transform(h)                    # warm
+                one = min((e.similarity_transform_ex(h) for _ in range(5)),
+                          key=lambda r: r[4]["loop_ms"])
+                loop = min((e.similarity_transform_ex(h, round_loop=True) for _ in range(5)),
+                           key=lambda r: r[4]["loop_ms"])
+                c0[name] = {"iter_count": one[3], "eigen_val": float(one[0]),
+                            "loop_ms_single_launch": round(one[4]["loop_ms"], 4),
+                            "loop_ms_round_launches": round(loop[4]["loop_ms"], 4)}
+        out["reference_headline"]["config0_hilbert128_gpu"] = c0
 
     # ---- CPU baseline (rank 0, N = 1) ------------------------------------
     if world == 1 and rank == 0 and not args.no_cpu:
