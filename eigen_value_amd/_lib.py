@@ -20,6 +20,7 @@ ST_SEM_MAINPY = 1
 ST_FLAG_TIME_KERNELS = 1
 ST_FLAG_MATRIX_FREE = 2
 ST_FLAG_ROUND_LOOP = 4
+ST_FLAG_WRITE_EVERY_ROUND = 8
 ST_MAX_ITR = 1000
 
 DTYPE_F32 = 0

@@ -801,15 +801,37 @@ flat_reverse(uint32_t b, uint32_t g)
   }
 }
 
+// Deferred writes (MAXP > 0): the matrix is stored only every few rounds.
+// A round that does not store still computes A_{k+1} = D_k^-1 A_k D_k in
+// registers and sums it into s_{k+1}; the next round re-reads the last
+// STORED matrix A_j and first re-applies the pending rounds' scalings
+// j .. k-1 - the same products, in the same order, as those rounds - so
+// every value (A, s, v, the stop decisions) is bit-identical to storing
+// every round, while a group of m rounds moves (m + 1) N^2 b instead of
+// 2 m N^2 b.  s[i] are s_j .. s_{k-1} (oldest first), n of them, and
+// inv[i] their reciprocals 1 / s (written by k_parts / k_recip, the same
+// correctly rounded quotient the round computed), so re-applying a round
+// costs two multiplies per element and no division.
+template <typename T, int MAXP>
+struct FlatPending
+{
+  const T* s[MAXP > 0 ? MAXP : 1];
+  const T* inv[MAXP > 0 ? MAXP : 1];
+  const T* inv_cur; // 1 / s_k (the current round's row scales)
+  uint32_t n;       // pending rounds (0 .. MAXP)
+  uint32_t store;   // store A_{k+1} this round
+};
+
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain>
+          int GATE = kGatePlain, int MAXP = 0>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
-       uint32_t col0 = 0, uint32_t col1 = 0)
+       uint32_t col0 = 0, uint32_t col1 = 0,
+       FlatPending<T, MAXP> pend = FlatPending<T, MAXP>{})
 {
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
   // columns [col0, col1) whose scales this rank computed itself, over the
@@ -864,13 +886,32 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     acc[j] = (T)0;
     if (in && r0 + j < nrows)
       x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
-    sr[j] = r0 + j < nrows ? s_cur[row0 + r0 + j] : (T)1;
+    // s_k[r], or with deferred writes already 1 / s_k[r]
+    const T* rs = MAXP > 0 ? pend.inv_cur : s_cur;
+    sr[j] = r0 + j < nrows ? rs[row0 + r0 + j] : (T)1;
   }
   // the piece's column scales, issued with the matrix loads (the stats of
   // the first row group read them too)
   V sc;
   if (in_cols)
     sc = *reinterpret_cast<const V*>(s_cur + c);
+  // deferred writes: the pending rounds' scales, issued with the matrix
+  // loads (a slot past n reads s_cur and is not applied)
+  V sp_c[MAXP > 0 ? MAXP : 1];
+  T sp_r[MAXP > 0 ? MAXP : 1][R]; // 1 / s_i[r]
+  if constexpr (MAXP > 0) {
+#pragma unroll
+    for (int i = 0; i < MAXP; i++) {
+      const bool live = i < (int)pend.n;
+      const T* sp = live ? pend.s[i] : s_cur;
+      const T* ip = live ? pend.inv[i] : s_cur;
+      if (in_cols)
+        sp_c[i] = *reinterpret_cast<const V*>(sp + c);
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        sp_r[i][j] = r0 + j < nrows ? ip[row0 + r0 + j] : (T)1;
+    }
+  }
   if constexpr (GATE == kGateSpec) {
     if (flat_gated<kGateAtomic>(state, k))
       return;
@@ -898,16 +939,35 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     }
   }
   if (in) {
+    if constexpr (MAXP > 0) {
+      // A_j -> A_k: the pending rounds' element updates, as they ran
+#pragma unroll
+      for (int i = 0; i < MAXP; i++) {
+        if (i < (int)pend.n) { // uniform
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            if (r0 + j < nrows) {
+              const T inv = sp_r[i][j];
+              if constexpr (ORDER == 0)
+                x[j] = x[j] * (inv * sp_c[i]);
+              else
+                x[j] = (inv * x[j]) * sp_c[i];
+            }
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int j = 0; j < R; j++) {
       if (r0 + j < nrows) {
-        const T inv = (T)1 / sr[j];
+        const T inv = MAXP > 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
           y = x[j] * (inv * sc); // cpp:324-325
         else
           y = (inv * x[j]) * sc; // main.py:13-16
-        st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c), y);
+        if (MAXP == 0 || pend.store)
+          st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c), y);
         acc[j] = hsum<T, W>(y);
       }
     }
@@ -978,12 +1038,14 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
         uint32_t ppr /* partials per row */, uint32_t k, const st_state* state,
         const T* __restrict__ s_cur = nullptr, T* __restrict__ v = nullptr,
         uint32_t row0 = 0, const T* __restrict__ part2 = nullptr,
-        uint32_t ppr2 = 0, uint32_t skip0 = 0, uint32_t nskip = 0)
+        uint32_t ppr2 = 0, uint32_t skip0 = 0, uint32_t nskip = 0,
+        T* __restrict__ inv_next = nullptr)
 {
   // [skip0, skip0 + nskip): parts of `part` not written (split round)
   // part2 (split round): the local half's partials, added after part's
   // v != nullptr: also v[r] *= s_k[r] / m_k (cpp:260) with m_k published by
   // k_flat's first row group
+  // inv_next != nullptr (deferred writes): also 1 / s_{k+1}[r]
   {
     const uint32_t e =
       __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1009,11 +1071,23 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   }
   if (lane == 0) {
     s_next[r] = acc;
+    if (inv_next != nullptr)
+      inv_next[r] = (T)1 / acc;
     if (v != nullptr) {
       const T m = (T)state->max;
       v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
     }
   }
+}
+
+// inv[i] = 1 / s[i] (the reciprocals of s_0 for deferred writes)
+template <typename T>
+__global__ __launch_bounds__(kBlock) void
+k_recip(const T* __restrict__ s, T* __restrict__ inv, uint32_t n)
+{
+  for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n;
+       i += gridDim.x * kBlock)
+    inv[i] = (T)1 / s[i];
 }
 
 // ---------------------------------------------------------------------------

@@ -53,6 +53,29 @@ int launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
                       st_state* st, hipStream_t stream);
 size_t round_flat_scratch(uint32_t nrows, uint32_t ncols);
 bool round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem);
+// the flat round with deferred writes (A stored every defer_rounds<T>() rounds,
+// bit-identical results; FlatPending in st_device.h): npend pending rounds'
+// s and 1/s (oldest first), inv_cur = 1/s_cur, inv_next <- 1/s_{k+1};
+// flush = store the matrix only (after the loop; no row sums, no v)
+// rounds per store: 3 in fp64, 4 in fp32 (profiles/r01_sweep_defer_ring.log)
+template <typename T>
+constexpr uint32_t
+defer_rounds()
+{
+  return sizeof(T) == 8 ? 3u : 4u;
+}
+constexpr uint32_t kDeferRoundsMax = 4;
+template <typename T>
+int launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur,
+                               T* s_next, T* inv_next, T* part, T* v,
+                               uint32_t nrows, uint32_t ncols, uint32_t row0,
+                               T eps, uint32_t k, uint32_t max_itr,
+                               uint32_t semantics, st_state* st,
+                               const T* const* pend_s,
+                               const T* const* pend_inv, uint32_t npend,
+                               bool store, bool flush, hipStream_t stream);
+template <typename T>
+int launch_recip(const T* s, T* inv, uint32_t n, hipStream_t stream);
 template <typename T>
 int launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
                  T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,

@@ -529,6 +529,121 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
   return check_launch("round_flat");
 }
 
+// ---- the flat round with deferred writes ----------------------------------
+// (FlatPending in st_device.h): A is stored every defer_rounds<T>() rounds;
+// the rounds in between re-apply the pending scalings from
+// the last stored matrix, bit-identical to storing every round.
+// tools/sweep_dir.hip SWEEP_DEFER=1 [SWEEP_DEFER_RING=1],
+// profiles/r01_sweep_defer{,_ring}.log, with s and 1/s in a ring of distinct
+// vectors as the solve keeps them: per round 32768^2 fp64 1.85 ms (every
+// 3rd round stored, 2 rows per workgroup) vs 2.70 storing every round,
+// 8192^2 fp64 0.125 vs 0.158; fp32 (every 4th, 4 rows) 0.821 vs 1.350 and
+// 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
+// registers outgrow the bytes saved.
+template <typename T, int W, int ORDER, bool NT>
+void
+launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
+                     T* inv_next, T* part, T* v, uint32_t nrows,
+                     uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+                     uint32_t max_itr, uint32_t semantics, st_state* st,
+                     const T* const* pend_s, const T* const* pend_inv,
+                     uint32_t npend, bool store, bool flush,
+                     hipStream_t stream)
+{
+  constexpr int MAXP = (int)defer_rounds<T>() - 1;
+  constexpr int R = sizeof(T) == 8 ? 2 : 4; // rows per workgroup
+  const uint32_t ppr = flat_pieces(ncols, W);
+  const uint32_t grid = (nrows + R - 1) / R * ppr;
+  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
+  dev::FlatPending<T, MAXP> pd{};
+  for (uint32_t i = 0; i < npend; i++) {
+    pd.s[i] = pend_s[i];
+    pd.inv[i] = pend_inv[i];
+  }
+  pd.inv_cur = inv_cur;
+  pd.n = npend;
+  pd.store = store ? 1u : 0u;
+  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
+                                  kBlock, 0, dev::kGatePlain, MAXP>),
+                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v,
+                     nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
+                     0u, 0u, 0u, pd);
+  if (!flush) // a flush only stores the matrix: s, v and the state stand
+    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
+                       part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
+                       0u, 0u, 0u, inv_next);
+}
+
+template <typename T>
+int
+launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
+                           T* inv_next, T* part, T* v, uint32_t nrows,
+                           uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+                           uint32_t max_itr, uint32_t semantics, st_state* st,
+                           const T* const* pend_s, const T* const* pend_inv,
+                           uint32_t npend, bool store, bool flush,
+                           hipStream_t stream)
+{
+  ST_REQUIRE(a && s_cur && inv_cur && part && v && st,
+             "round_flat_deferred: null pointer");
+  ST_REQUIRE(flush || (s_next && inv_next), "round_flat_deferred: null pointer");
+  ST_REQUIRE(npend < defer_rounds<T>(),
+             "round_flat_deferred: %u pending rounds", npend);
+  ST_REQUIRE(!flush || store, "round_flat_deferred: a flush stores");
+  ST_REQUIRE(ncols > 0 && nrows > 0 && row0 + (uint64_t)nrows <= ncols,
+             "round_flat_deferred: bad block");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "round_flat_deferred: bad semantics");
+  constexpr int W = 16 / sizeof(T);
+  bool vec_ok = (ncols % W) == 0 && aligned16(a) && aligned16(s_cur);
+  for (uint32_t i = 0; i < npend; i++)
+    vec_ok = vec_ok && aligned16(pend_s[i]);
+  const bool order1 = semantics == ST_SEM_MAINPY;
+  const bool nt = flat_round_nt(nrows, ncols, sizeof(T));
+#define ST_DEF(WW, OO, NN)                                                     \
+  launch_flat_deferred<T, WW, OO, NN>(a, s_cur, inv_cur, s_next, inv_next,     \
+                                      part, v, nrows, ncols, row0, eps, k,     \
+                                      max_itr, semantics, st, pend_s,          \
+                                      pend_inv, npend, store, flush, stream)
+  if (vec_ok) {
+    if (order1)
+      nt ? ST_DEF(W, 1, true) : ST_DEF(W, 1, false);
+    else
+      nt ? ST_DEF(W, 0, true) : ST_DEF(W, 0, false);
+  } else {
+    if (order1)
+      nt ? ST_DEF(1, 1, true) : ST_DEF(1, 1, false);
+    else
+      nt ? ST_DEF(1, 0, true) : ST_DEF(1, 0, false);
+  }
+#undef ST_DEF
+  return check_launch("round_flat_deferred");
+}
+
+template <typename T>
+int
+launch_recip(const T* s, T* inv, uint32_t n, hipStream_t stream)
+{
+  ST_REQUIRE(s && inv, "recip: null pointer");
+  const uint32_t grid = (n + kBlock - 1) / kBlock < 1024u ? (n + kBlock - 1) / kBlock
+                                                          : 1024u;
+  hipLaunchKernelGGL((dev::k_recip<T>), dim3(grid), dim3(kBlock), 0, stream, s,
+                     inv, n);
+  return check_launch("recip");
+}
+
+template int launch_round_flat_deferred<float>(
+  float*, const float*, const float*, float*, float*, float*, float*, uint32_t,
+  uint32_t, uint32_t, float, uint32_t, uint32_t, uint32_t, st_state*,
+  const float* const*, const float* const*, uint32_t, bool, bool, hipStream_t);
+template int launch_round_flat_deferred<double>(
+  double*, const double*, const double*, double*, double*, double*, double*,
+  uint32_t, uint32_t, uint32_t, double, uint32_t, uint32_t, uint32_t,
+  st_state*, const double* const*, const double* const*, uint32_t, bool, bool,
+  hipStream_t);
+template int launch_recip<float>(const float*, float*, uint32_t, hipStream_t);
+template int launch_recip<double>(const double*, double*, uint32_t,
+                                  hipStream_t);
+
 // ---- the flat round split in two for the overlapped exchange ------------
 // span 1 (local): k_flat over the pieces holding [col0, col1), lanes masked
 // to those columns, partials to the local region of `part`; span 2

@@ -63,7 +63,9 @@ struct Context
   // cached device workspaces (grown on demand, freed by destroy_queue)
   void* d_mat = nullptr;
   size_t mat_bytes = 0;
-  void* d_vec = nullptr; // [s0 | s1 | v | v'], each vec_bytes
+  // [s0 | s1 | v | v' | s ring (kDeferRoundsMax + 1) | 1/s ring (same)],
+  // each vec_bytes
+  void* d_vec = nullptr;
   size_t vec_bytes = 0;
   void* d_part = nullptr; // flat-round partial sums (large matrices)
   size_t part_bytes = 0;
@@ -99,7 +101,7 @@ ensure_vectors(Context* c, size_t vec_bytes)
     ST_CHECK(hipFree(c->d_vec));
     c->d_vec = nullptr;
   }
-  ST_CHECK(hipMalloc(&c->d_vec, 4 * vec_bytes));
+  ST_CHECK(hipMalloc(&c->d_vec, (4 + 2 * (kDeferRoundsMax + 1)) * vec_bytes));
   c->vec_bytes = vec_bytes;
   return 0;
 }
@@ -173,11 +175,13 @@ resolve(const st_options* opt, Resolved* r)
 }
 
 // The round loop on a device-resident matrix (transformed in place).
+// flush_matrix: leave the matrix as the every-round loop would (the caller
+// sees it); a private copy (solve_host) skips the deferred loop's last store
 template <typename T>
 int64_t
 solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
              T* eigen_val, uint32_t* iter_cnt, const st_options* opt,
-             st_stats* stats)
+             st_stats* stats, bool flush_matrix = true)
 {
   ST_REQUIRE(c, "null queue");
   ST_REQUIRE(d_mat, "null matrix");
@@ -201,6 +205,18 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
   // large matrices: the flat round (k_flat + k_parts)
   const bool flat = !mfree && round_flat_pays(n, n, sizeof(T));
+  // the flat round stores the matrix every kDefer rounds (bit-identical
+  // results; ST_FLAG_WRITE_EVERY_ROUND stores every round)
+  const bool defer = flat && (o.flags & ST_FLAG_WRITE_EVERY_ROUND) == 0;
+  constexpr uint32_t kDefer = defer_rounds<T>();
+  constexpr uint32_t kR = kDefer + 1; // ring slots: pending + s_k + s_{k+1}
+  T* ring_s[kR];
+  T* ring_inv[kR];
+  for (uint32_t i = 0; i < kR; i++) {
+    ring_s[i] = reinterpret_cast<T*>((char*)c->d_vec + (4 + i) * c->vec_bytes);
+    ring_inv[i] = reinterpret_cast<T*>((char*)c->d_vec +
+                                       (4 + kDeferRoundsMax + 1 + i) * c->vec_bytes);
+  }
   if (flat && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
     return -1;
   T* d_part = reinterpret_cast<T*>(c->d_part);
@@ -244,7 +260,9 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
       return -1;
     (void)hipEventRecord(ev[0], s);
   }
-  if (!single && launch_rowsum<T>(d_mat, s_buf[0], n, n, s)) // K0
+  if (!single && launch_rowsum<T>(d_mat, defer ? ring_s[0] : s_buf[0], n, n, s)) // K0
+    return -1;
+  if (defer && launch_recip<T>(ring_s[0], ring_inv[0], n, s))
     return -1;
   if (timed)
     (void)hipEventRecord(ev[1], s);
@@ -274,7 +292,20 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
         rc |= launch_mfree<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], vb[k & 1],
                               vb[(k + 1) & 1], n, n, 0, eps, k + 1, o.max_itr,
                               o.semantics, c->d_state, s);
-      else if (flat)
+      else if (defer) {
+        // stored: A_j, j = the last multiple of kDefer <= k
+        const uint32_t j0 = k - k % kDefer, np = k - j0;
+        const T* ps[kDefer];
+        const T* pi[kDefer];
+        for (uint32_t i = 0; i < np; i++) {
+          ps[i] = ring_s[(j0 + i) % kR];
+          pi[i] = ring_inv[(j0 + i) % kR];
+        }
+        rc |= launch_round_flat_deferred<T>(
+          d_mat, ring_s[k % kR], ring_inv[k % kR], ring_s[(k + 1) % kR],
+          ring_inv[(k + 1) % kR], d_part, d_v, n, n, 0, eps, k, o.max_itr,
+          o.semantics, c->d_state, ps, pi, np, np + 1 == kDefer, false, s);
+      } else if (flat)
         rc |= launch_round_flat<T>(d_mat, s_buf[cur], s_buf[cur ^ 1], d_part,
                                    d_v, n, n, 0, eps, k, o.max_itr,
                                    o.semantics, c->d_state, s);
@@ -303,6 +334,23 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   st_state fin;
   ST_CHECK(hipMemcpy(&fin, c->d_state, sizeof(st_state), hipMemcpyDeviceToHost));
   ST_REQUIRE(fin.done, "internal: loop ended without done flag");
+  if (defer && flush_matrix && fin.end % kDefer != 0) {
+    // the matrix stands at A_J (J = the last store); apply rounds J .. end-1
+    // and store A_end, exactly what storing every round leaves
+    const uint32_t kl = fin.end - 1, j0 = kl - kl % kDefer, np = kl - j0;
+    const T* ps[kDefer];
+    const T* pi[kDefer];
+    for (uint32_t i = 0; i < np; i++) {
+      ps[i] = ring_s[(j0 + i) % kR];
+      pi[i] = ring_inv[(j0 + i) % kR];
+    }
+    if (launch_round_flat_deferred<T>(
+          d_mat, ring_s[kl % kR], ring_inv[kl % kR], nullptr, nullptr, d_part,
+          d_v, n, n, 0, eps, kl, o.max_itr, o.semantics, c->d_state, ps, pi,
+          np, true, true, s))
+      return -1;
+    ST_CHECK(hipStreamSynchronize(s));
+  }
   if (mfree && (fin.end & 1u)) { // the final v_{end-1} landed in the partner
     ST_CHECK(hipMemcpyAsync(d_v, d_v2, sizeof(T) * (size_t)n,
                             hipMemcpyDeviceToDevice, s));
@@ -369,7 +417,8 @@ solve_host(Context* c, const T* mat, uint32_t n, T* eigen_val, T* eigen_vec,
   const double h2d = ms_since(t0);
   st_stats local{};
   if (solve_device<T>(c, reinterpret_cast<T*>(c->d_mat), n, nullptr,
-                      eigen_vec, eigen_val, iter_cnt, opt, &local) < 0)
+                      eigen_vec, eigen_val, iter_cnt, opt, &local,
+                      false) < 0)
     return -1;
   local.h2d_ms = h2d;
   if (stats)

@@ -267,12 +267,16 @@ class DeviceSolver:
     def solve(self, mat, *, inplace: bool = False, eps: Optional[float] = None,
               max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL, batch: int = 0,
               time_kernels: bool = False, matrix_free: bool = False,
-              round_loop: bool = False):
+              round_loop: bool = False, write_every_round: bool = False):
         """Returns (λ: float, v: tensor, iterations: int, stats: dict).
 
         Matrices of n <= 128 (fp64) / 256 (fp32) run the whole solve in one
         workgroup launch (bit-identical); ``round_loop`` forces one launch per
-        round instead (``ST_FLAG_ROUND_LOOP``).
+        round instead (``ST_FLAG_ROUND_LOOP``).  Matrices of >= 144 MiB
+        store the transformed matrix every 3rd round and re-apply the pending
+        scalings in registers (identical results and final matrix, a third
+        fewer bytes); ``write_every_round`` stores it every round
+        (``ST_FLAG_WRITE_EVERY_ROUND``).
 
         ``mat`` is transformed in place when ``inplace`` (it is the private
         working copy the reference makes, similarity_transform.cpp:14,19).
@@ -297,7 +301,8 @@ class DeviceSolver:
         it = ctypes.c_uint32()
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
                  | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
-                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0))
+                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0)
+                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()

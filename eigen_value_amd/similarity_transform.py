@@ -75,10 +75,14 @@ class EigenValue:
     def similarity_transform_ex(self, mat: np.ndarray, *, eps: Optional[float] = None,
                                 max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL,
                                 batch: int = 0, time_kernels: bool = False,
-                                matrix_free: bool = False, round_loop: bool = False):
+                                matrix_free: bool = False, round_loop: bool = False,
+                                write_every_round: bool = False):
         """Extended call: options + statistics (``max_eigen_value_ex``).
         ``round_loop`` keeps one launch per round where the whole solve would
-        fit one workgroup (``ST_FLAG_ROUND_LOOP``; identical results).
+        fit one workgroup (``ST_FLAG_ROUND_LOOP``; identical results);
+        ``write_every_round`` stores the matrix every round where the flat
+        round would store it every 3rd (``ST_FLAG_WRITE_EVERY_ROUND``;
+        identical results).
 
         Returns ``(λ, v, ts_ms, iterations, stats_dict)``."""
         m, n = mat.shape
@@ -88,7 +92,8 @@ class EigenValue:
             raise TypeError("float32 or float64 matrix required")
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
                  | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
-                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0))
+                 | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0)
+                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()

@@ -90,6 +90,11 @@ typedef struct st_options
 #define ST_FLAG_TIME_KERNELS 1u /* hipEvents around every fused launch     */
 #define ST_FLAG_MATRIX_FREE 2u  /* st_mfree_round_* instead of the in-place */
                                 /* transform (input never written)         */
+#define ST_FLAG_WRITE_EVERY_ROUND 8u /* store the matrix every round; by    */
+                                /* default the flat round (>= 144 MiB)      */
+                                /* stores it every 3rd round and re-applies */
+                                /* the pending scalings in registers:       */
+                                /* identical results, fewer bytes           */
 #define ST_FLAG_ROUND_LOOP 4u   /* one launch per round even where the whole */
                                 /* solve fits one workgroup (n <= 128 fp64, */
                                 /* 256 fp32): results are identical        */

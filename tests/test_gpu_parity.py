@@ -993,3 +993,36 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
                     for _ in range(5))
     print(f"hilbert128 f32 loop_ms: single launch {best:.4f}, per round {best_loop:.4f}")
     assert best < best_loop
+
+
+# ---------------------------------------------------------------------------
+# deferred writes (blocks >= 144 MiB: the flat round stores A every 3rd round
+# and re-applies the pending scalings) against storing every round:
+# bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144)])
+@pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
+def test_deferred_writes_bitwise(solver, dt, n, sem):
+    assert dev.flat_round_pays(n, n, TD[dt])
+    base = dev.generate("random", n, TD[dt], seed=4, device=DEV)
+    # fixed round counts ending at every residue mod 3 (the final flush), a
+    # converging solve, and max_itr = 1
+    for kw in (dict(eps=0.0, max_itr=7), dict(eps=0.0, max_itr=8), dict(eps=0.0, max_itr=9),
+               dict(), dict(eps=1e-9), dict(max_itr=1)):
+        a1, a2 = base.clone(), base.clone()
+        r1 = solver.solve(a1, inplace=True, semantics=sem, **kw)
+        r2 = solver.solve(a2, inplace=True, semantics=sem, write_every_round=True, **kw)
+        assert (r1[0], r1[2], r1[3]["rounds"], r1[3]["converged"]) == \
+               (r2[0], r2[2], r2[3]["rounds"], r2[3]["converged"]), kw
+        assert torch.equal(r1[1], r2[1]), kw                # v bitwise
+        assert torch.equal(a1, a2), kw                      # final matrix bitwise
+
+
+def test_deferred_writes_dropin_and_batches(eigen, orc):
+    # the host-matrix path (private copy, no final flush) and batch sizes
+    # that stop mid-group: identical to storing every round
+    mat = orc.hilbert(6144, np.float32)
+    ref = eigen.similarity_transform_ex(mat, write_every_round=True)
+    for batch in (1, 2, 5):
+        got = eigen.similarity_transform_ex(mat, batch=batch)
+        assert got[0] == ref[0] and np.array_equal(got[1], ref[1]) and got[3] == ref[3]

@@ -257,6 +257,57 @@ round_lib(const Bufs<T>& b)
               bytes / (t * 1e-3) / 1e9);
 }
 
+// the flat round with deferred writes: A stored every m = MAXP + 1 rounds,
+// the rounds in between re-apply the pending scalings in registers; the
+// time per round averaged over the 16-round sequence
+template <typename T, bool NT, int MAXP, int R = 2, bool RING = false>
+static void
+defer_seq(const Bufs<T>& b, T* part)
+{
+  // RING: s / 1/s in a ring of M + 1 distinct vectors as the solve loop
+  // keeps them (otherwise every slot is the same vector)
+  constexpr int W = 16 / sizeof(T);
+  constexpr int M = MAXP + 1;
+  const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
+  const unsigned grid = (b.nr + R - 1) / R * ppr;
+  T* ring = nullptr;
+  HIPCHECK(hipMalloc(&ring, sizeof(T) * (size_t)b.n * 2 * (M + 1)));
+  for (int i = 0; i <= M; i++) {
+    HIPCHECK(hipMemcpy(ring + (size_t)i * b.n, b.s, sizeof(T) * b.n,
+                       hipMemcpyDeviceToDevice));
+    hipLaunchKernelGGL((k_recip<T>), dim3(64), dim3(256), 0, 0, b.s,
+                       ring + (size_t)(M + 1 + i) * b.n, b.n);
+  }
+  auto rs = [&](int i) { return RING ? ring + (size_t)(i % (M + 1)) * b.n : ring; };
+  auto ri = [&](int i) {
+    return RING ? ring + (size_t)(M + 1 + i % (M + 1)) * b.n : ring + (size_t)(M + 1) * b.n;
+  };
+  float t = time_seq([&](int k) {
+    FlatPending<T, MAXP> pend{};
+    const int j0 = k - k % M;
+    pend.n = (uint32_t)(k % M);
+    for (int i = 0; i < MAXP; i++) {
+      pend.s[i] = rs(j0 + i);
+      pend.inv[i] = ri(j0 + i);
+    }
+    pend.inv_cur = ri(k);
+    pend.store = (k % M) == M - 1 ? 1u : 0u;
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0,
+                                kGatePlain, MAXP>),
+                       dim3(grid), dim3(256), 0, 0, b.a, rs(k), part, b.v, b.nr,
+                       b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u,
+                       0u, 0u, pend);
+    hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
+                       part, b.sn, b.nr, ppr, (uint32_t)k, b.st, rs(k), b.v, 0u,
+                       nullptr, 0u, 0u, 0u, (T*)nullptr);
+  });
+  HIPCHECK(hipFree(ring));
+  const double bytes = (double)(M + 1) / M * b.nr * (double)b.n * sizeof(T);
+  std::printf("  defer m=%d r=%d ring=%d nt=%d  per round %8.4f ms  (%.3f N^2 b per round) "
+              "%7.1f GB/s\n",
+              M, R, (int)RING, (int)NT, t, (double)(M + 1) / M, bytes / (t * 1e-3) / 1e9);
+}
+
 template <typename T>
 static void
 round_ref(const Bufs<T>& b, int rows_round, unsigned cap_round)
@@ -352,6 +403,60 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_DEFER")) { // deferred writes: store A every m rounds
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    const bool ring_only = std::getenv("SWEEP_DEFER_RING") != nullptr;
+    for (int rep = 0; rep < 2; rep++) {
+      if (big) {
+        flat2_seq<T, 2, true, 2, 256, kGatePlain>(b, part);
+        if (!ring_only) {
+          defer_seq<T, true, 1>(b, part);
+          defer_seq<T, true, 2>(b, part);
+          defer_seq<T, true, 3>(b, part);
+          defer_seq<T, true, 5>(b, part);
+          defer_seq<T, true, 7>(b, part);
+          defer_seq<T, true, 11>(b, part);
+        } else {
+          defer_seq<T, true, 2, 2, false>(b, part);
+          defer_seq<T, true, 1, 2, true>(b, part);
+          defer_seq<T, true, 2, 2, true>(b, part);
+          defer_seq<T, true, 3, 2, true>(b, part);
+          defer_seq<T, true, 1, 4, true>(b, part);
+          defer_seq<T, true, 2, 4, true>(b, part);
+          defer_seq<T, true, 3, 4, true>(b, part);
+        }
+      } else {
+        flat2_seq<T, 2, false, 2, 256, kGatePlain>(b, part);
+        if (!ring_only) {
+          defer_seq<T, false, 1>(b, part);
+          defer_seq<T, false, 2>(b, part);
+          defer_seq<T, false, 3>(b, part);
+          defer_seq<T, false, 5>(b, part);
+          defer_seq<T, false, 7>(b, part);
+          defer_seq<T, false, 11>(b, part);
+        } else {
+          defer_seq<T, false, 2, 2, false>(b, part);
+          defer_seq<T, false, 1, 2, true>(b, part);
+          defer_seq<T, false, 2, 2, true>(b, part);
+          defer_seq<T, false, 3, 2, true>(b, part);
+          defer_seq<T, false, 1, 4, true>(b, part);
+          defer_seq<T, false, 2, 4, true>(b, part);
+          defer_seq<T, false, 3, 4, true>(b, part);
+        }
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_PARTS")) { // k_parts: one wave vs one thread per row
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
