@@ -27,7 +27,12 @@ the launch stream), `cpu_baseline` (the CPU oracle's 3-pass schedule on
 the host cores, rank 0 at N=1), `solve` (the reference-semantics solve to
 convergence: rounds, λ), `matrix_free` (the read-only form of the same
 iteration, SURVEY.md §8f item 1, priced against its own N^2*b bytes),
-`north_star` (32768x32768 random fp64, 1 GPU, both forms).
+`north_star` (32768x32768 random fp64, 1 GPU, both forms),
+`deferred_writes` (the library's solve loop, which stores the matrix every
+3rd fp64 / 4th fp32 round with bit-identical results, against storing every
+round; priced against its own (m+1)/m*N^2*b bytes) and, under
+`reference_headline`, `config0_hilbert128_gpu` (configs[0]'s 128^2 Hilbert
+solved on the GPU in one workgroup launch).
 """
 from __future__ import annotations
 
