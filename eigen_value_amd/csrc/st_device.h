@@ -801,37 +801,38 @@ flat_reverse(uint32_t b, uint32_t g)
   }
 }
 
-// Deferred writes (MAXP > 0): the matrix is stored only every few rounds.
+// Deferred writes (NP >= 0): the matrix is stored only every few rounds.
 // A round that does not store still computes A_{k+1} = D_k^-1 A_k D_k in
 // registers and sums it into s_{k+1}; the next round re-reads the last
 // STORED matrix A_j and first re-applies the pending rounds' scalings
 // j .. k-1 - the same products, in the same order, as those rounds - so
 // every value (A, s, v, the stop decisions) is bit-identical to storing
 // every round, while a group of m rounds moves (m + 1) N^2 b instead of
-// 2 m N^2 b.  s[i] are s_j .. s_{k-1} (oldest first), n of them, and
-// inv[i] their reciprocals 1 / s (written by k_parts / k_recip, the same
-// correctly rounded quotient the round computed), so re-applying a round
-// costs two multiplies per element and no division.
-template <typename T, int MAXP>
+// 2 m N^2 b.  s[i] are s_j .. s_{k-1} (oldest first), NP = k - j of them
+// (a template argument: no runtime selects between the kernel arguments and
+// the loads they address), and inv[i] their reciprocals 1 / s (written by
+// k_parts / k_recip, the same correctly rounded quotient the round
+// computed), so re-applying a round costs two multiplies per element and no
+// division.
+template <typename T, int NP>
 struct FlatPending
 {
-  const T* s[MAXP > 0 ? MAXP : 1];
-  const T* inv[MAXP > 0 ? MAXP : 1];
+  const T* s[NP > 0 ? NP : 1];
+  const T* inv[NP > 0 ? NP : 1];
   const T* inv_cur; // 1 / s_k (the current round's row scales)
-  uint32_t n;       // pending rounds (0 .. MAXP)
   uint32_t store;   // store A_{k+1} this round
 };
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain, int MAXP = 0>
+          int GATE = kGatePlain, int NP = -1>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
-       FlatPending<T, MAXP> pend = FlatPending<T, MAXP>{})
+       FlatPending<T, NP> pend = FlatPending<T, NP>{})
 {
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
   // columns [col0, col1) whose scales this rank computed itself, over the
@@ -887,7 +888,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     if (in && r0 + j < nrows)
       x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
     // s_k[r], or with deferred writes already 1 / s_k[r]
-    const T* rs = MAXP > 0 ? pend.inv_cur : s_cur;
+    const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
     sr[j] = r0 + j < nrows ? rs[row0 + r0 + j] : (T)1;
   }
   // the piece's column scales, issued with the matrix loads (the stats of
@@ -896,20 +897,17 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   if (in_cols)
     sc = *reinterpret_cast<const V*>(s_cur + c);
   // deferred writes: the pending rounds' scales, issued with the matrix
-  // loads (a slot past n reads s_cur and is not applied)
-  V sp_c[MAXP > 0 ? MAXP : 1];
-  T sp_r[MAXP > 0 ? MAXP : 1][R]; // 1 / s_i[r]
-  if constexpr (MAXP > 0) {
+  // loads
+  V sp_c[NP > 0 ? NP : 1];
+  T sp_r[NP > 0 ? NP : 1][R]; // 1 / s_i[r]
+  if constexpr (NP > 0) {
 #pragma unroll
-    for (int i = 0; i < MAXP; i++) {
-      const bool live = i < (int)pend.n;
-      const T* sp = live ? pend.s[i] : s_cur;
-      const T* ip = live ? pend.inv[i] : s_cur;
+    for (int i = 0; i < NP; i++) {
       if (in_cols)
-        sp_c[i] = *reinterpret_cast<const V*>(sp + c);
+        sp_c[i] = *reinterpret_cast<const V*>(pend.s[i] + c);
 #pragma unroll
       for (int j = 0; j < R; j++)
-        sp_r[i][j] = r0 + j < nrows ? ip[row0 + r0 + j] : (T)1;
+        sp_r[i][j] = r0 + j < nrows ? pend.inv[i][row0 + r0 + j] : (T)1;
     }
   }
   if constexpr (GATE == kGateSpec) {
@@ -939,20 +937,18 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     }
   }
   if (in) {
-    if constexpr (MAXP > 0) {
+    if constexpr (NP > 0) {
       // A_j -> A_k: the pending rounds' element updates, as they ran
 #pragma unroll
-      for (int i = 0; i < MAXP; i++) {
-        if (i < (int)pend.n) { // uniform
+      for (int i = 0; i < NP; i++) {
 #pragma unroll
-          for (int j = 0; j < R; j++) {
-            if (r0 + j < nrows) {
-              const T inv = sp_r[i][j];
-              if constexpr (ORDER == 0)
-                x[j] = x[j] * (inv * sp_c[i]);
-              else
-                x[j] = (inv * x[j]) * sp_c[i];
-            }
+        for (int j = 0; j < R; j++) {
+          if (r0 + j < nrows) {
+            const T inv = sp_r[i][j];
+            if constexpr (ORDER == 0)
+              x[j] = x[j] * (inv * sp_c[i]);
+            else
+              x[j] = (inv * x[j]) * sp_c[i];
           }
         }
       }
@@ -960,13 +956,13 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
     for (int j = 0; j < R; j++) {
       if (r0 + j < nrows) {
-        const T inv = MAXP > 0 ? sr[j] : (T)1 / sr[j];
+        const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
           y = x[j] * (inv * sc); // cpp:324-325
         else
           y = (inv * x[j]) * sc; // main.py:13-16
-        if (MAXP == 0 || pend.store)
+        if (NP < 0 || pend.store)
           st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c), y);
         acc[j] = hsum<T, W>(y);
       }

@@ -540,6 +540,37 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 8192^2 fp64 0.125 vs 0.158; fp32 (every 4th, 4 rows) 0.821 vs 1.350 and
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
+template <typename T, int W, int ORDER, bool NT, int NP>
+void
+launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
+                        T* inv_next, T* part, T* v, uint32_t nrows,
+                        uint32_t ncols, uint32_t row0, T eps, uint32_t k,
+                        uint32_t max_itr, uint32_t semantics, st_state* st,
+                        const T* const* pend_s, const T* const* pend_inv,
+                        bool store, bool flush, hipStream_t stream)
+{
+  constexpr int R = sizeof(T) == 8 ? 2 : 4; // rows per workgroup
+  const uint32_t ppr = flat_pieces(ncols, W);
+  const uint32_t grid = (nrows + R - 1) / R * ppr;
+  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
+  dev::FlatPending<T, NP> pd{};
+  for (int i = 0; i < NP; i++) {
+    pd.s[i] = pend_s[i];
+    pd.inv[i] = pend_inv[i];
+  }
+  pd.inv_cur = inv_cur;
+  pd.store = store ? 1u : 0u;
+  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
+                                  kBlock, 0, dev::kGatePlain, NP>),
+                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v,
+                     nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
+                     0u, 0u, 0u, pd);
+  if (!flush) // a flush only stores the matrix: s, v and the state stand
+    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
+                       part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
+                       0u, 0u, 0u, inv_next);
+}
+
 template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
@@ -550,28 +581,20 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
-  constexpr int MAXP = (int)defer_rounds<T>() - 1;
-  constexpr int R = sizeof(T) == 8 ? 2 : 4; // rows per workgroup
-  const uint32_t ppr = flat_pieces(ncols, W);
-  const uint32_t grid = (nrows + R - 1) / R * ppr;
-  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
-  dev::FlatPending<T, MAXP> pd{};
-  for (uint32_t i = 0; i < npend; i++) {
-    pd.s[i] = pend_s[i];
-    pd.inv[i] = pend_inv[i];
+#define ST_NP(NPV)                                                             \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV>(                               \
+    a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
+    max_itr, semantics, st, pend_s, pend_inv, store, flush, stream)
+  switch (npend) {
+  case 0: ST_NP(0); break;
+  case 1: ST_NP(1); break;
+  case 2: ST_NP(2); break;
+  default:
+    if constexpr (defer_rounds<T>() > 3)
+      ST_NP(3);
+    break;
   }
-  pd.inv_cur = inv_cur;
-  pd.n = npend;
-  pd.store = store ? 1u : 0u;
-  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
-                                  kBlock, 0, dev::kGatePlain, MAXP>),
-                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v,
-                     nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
-                     0u, 0u, 0u, pd);
-  if (!flush) // a flush only stores the matrix: s, v and the state stand
-    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
-                       part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
-                       0u, 0u, 0u, inv_next);
+#undef ST_NP
 }
 
 template <typename T>

@@ -260,12 +260,32 @@ round_lib(const Bufs<T>& b)
 // the flat round with deferred writes: A stored every m = MAXP + 1 rounds,
 // the rounds in between re-apply the pending scalings in registers; the
 // time per round averaged over the 16-round sequence
+template <typename T, bool NT, int R, int NP>
+static void
+defer_launch(const Bufs<T>& b, T* part, unsigned ppr, unsigned grid, int k,
+             const T* s_cur, const T* inv_cur, T* const* ps, T* const* pi,
+             bool store)
+{
+  constexpr int W = 16 / sizeof(T);
+  FlatPending<T, NP> pend{};
+  for (int i = 0; i < NP; i++) {
+    pend.s[i] = ps[i];
+    pend.inv[i] = pi[i];
+  }
+  pend.inv_cur = inv_cur;
+  pend.store = store ? 1u : 0u;
+  hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NP>),
+                     dim3(grid), dim3(256), 0, 0, b.a, s_cur, part, b.v, b.nr, b.n,
+                     ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pend);
+}
+
 template <typename T, bool NT, int MAXP, int R = 2, bool RING = false>
 static void
 defer_seq(const Bufs<T>& b, T* part)
 {
   // RING: s / 1/s in a ring of M + 1 distinct vectors as the solve loop
   // keeps them (otherwise every slot is the same vector)
+  static_assert(MAXP <= 3, "pending rounds");
   constexpr int W = 16 / sizeof(T);
   constexpr int M = MAXP + 1;
   const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
@@ -283,20 +303,20 @@ defer_seq(const Bufs<T>& b, T* part)
     return RING ? ring + (size_t)(M + 1 + i % (M + 1)) * b.n : ring + (size_t)(M + 1) * b.n;
   };
   float t = time_seq([&](int k) {
-    FlatPending<T, MAXP> pend{};
-    const int j0 = k - k % M;
-    pend.n = (uint32_t)(k % M);
-    for (int i = 0; i < MAXP; i++) {
-      pend.s[i] = rs(j0 + i);
-      pend.inv[i] = ri(j0 + i);
+    const int j0 = k - k % M, np = k % M;
+    T* ps[4];
+    T* pi[4];
+    for (int i = 0; i < np; i++) {
+      ps[i] = rs(j0 + i);
+      pi[i] = ri(j0 + i);
     }
-    pend.inv_cur = ri(k);
-    pend.store = (k % M) == M - 1 ? 1u : 0u;
-    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0,
-                                kGatePlain, MAXP>),
-                       dim3(grid), dim3(256), 0, 0, b.a, rs(k), part, b.v, b.nr,
-                       b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u,
-                       0u, 0u, pend);
+    const bool store = np == M - 1;
+    switch (np) {
+    case 0: defer_launch<T, NT, R, 0>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
+    case 1: defer_launch<T, NT, R, 1>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
+    case 2: defer_launch<T, NT, R, 2>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
+    default: defer_launch<T, NT, R, 3>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
+    }
     hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
                        part, b.sn, b.nr, ppr, (uint32_t)k, b.st, rs(k), b.v, 0u,
                        nullptr, 0u, 0u, 0u, (T*)nullptr);
@@ -416,9 +436,6 @@ run(unsigned nr, unsigned n)
           defer_seq<T, true, 1>(b, part);
           defer_seq<T, true, 2>(b, part);
           defer_seq<T, true, 3>(b, part);
-          defer_seq<T, true, 5>(b, part);
-          defer_seq<T, true, 7>(b, part);
-          defer_seq<T, true, 11>(b, part);
         } else {
           defer_seq<T, true, 2, 2, false>(b, part);
           defer_seq<T, true, 1, 2, true>(b, part);
@@ -434,9 +451,6 @@ run(unsigned nr, unsigned n)
           defer_seq<T, false, 1>(b, part);
           defer_seq<T, false, 2>(b, part);
           defer_seq<T, false, 3>(b, part);
-          defer_seq<T, false, 5>(b, part);
-          defer_seq<T, false, 7>(b, part);
-          defer_seq<T, false, 11>(b, part);
         } else {
           defer_seq<T, false, 2, 2, false>(b, part);
           defer_seq<T, false, 1, 2, true>(b, part);
