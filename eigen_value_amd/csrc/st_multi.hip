@@ -4,9 +4,12 @@
 //
 // Device d owns rows [d*chunk, d*chunk + rows_d), chunk = ceil(N/P), and
 // keeps: its row block of A (transformed in place, or read only in the
-// matrix-free form), two padded P*chunk row-sum vectors (ping-pong), the
-// eigenvector accumulator(s) and an st_state.  Round k on every device:
-//   k_round  (or k_mfree, launch k+1) on its stream      st_device.h
+// matrix-free form), a ring of padded P*chunk row-sum vectors (two slots,
+// or defer_rounds + 1 when its block takes the flat round with deferred
+// writes, with their reciprocals), the eigenvector accumulator(s) and an
+// st_state.  Round k on every device:
+//   k_round / the flat round (deferred writes: A stored every 3rd fp64 /
+//   4th fp32 round, st_solve.hip) / k_mfree (launch k+1) on its stream
 //   ncclAllGather(slot_d, s_next, chunk, type, comm_d, stream_d)
 // Every device derives m_k / stop_k from the identical gathered vector, so
 // the states agree without a further collective; the host polls device 0's
@@ -63,9 +66,11 @@ struct Shard
   hipStream_t stream = nullptr;
   ncclComm_t comm = nullptr;
   T* a = nullptr;
-  T* s[2] = { nullptr, nullptr };
+  T* s[kDeferRoundsMax + 1] = {};   // row sums, ring slot k % nring
+  T* inv[kDeferRoundsMax + 1] = {}; // 1 / s (deferred writes only)
   T* v[2] = { nullptr, nullptr };
   T* part = nullptr; // flat-round partial sums (large blocks)
+  bool defer = false; // the flat round with deferred writes
   st_state* state = nullptr;
 };
 
@@ -84,10 +89,12 @@ struct Multi
       if (d.comm)
         (void)ncclCommDestroy(d.comm);
       (void)hipFree(d.a);
-      for (int i = 0; i < 2; i++) {
+      for (uint32_t i = 0; i <= kDeferRoundsMax; i++) {
         (void)hipFree(d.s[i]);
-        (void)hipFree(d.v[i]);
+        (void)hipFree(d.inv[i]);
       }
+      for (int i = 0; i < 2; i++)
+        (void)hipFree(d.v[i]);
       (void)hipFree(d.part);
       (void)hipFree(d.state);
       if (d.stream)
@@ -145,7 +152,18 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   const uint32_t sem = opt ? opt->semantics : ST_SEM_SYCL;
   uint32_t batch = (opt && opt->batch) ? opt->batch : 0u;
   const bool mfree = opt && (opt->flags & ST_FLAG_MATRIX_FREE);
+  const bool every = opt && (opt->flags & ST_FLAG_WRITE_EVERY_ROUND);
   ST_REQUIRE(sem <= ST_SEM_MAINPY, "unknown semantics %u", sem);
+  // ring slots of the row-sum vectors: every shard gathers into the same
+  // slot, so the ring is as long as the longest any shard needs
+  bool defer_any = false;
+  for (uint32_t p = 0; p < P; p++) {
+    const uint32_t r0 = p * ((n + P - 1) / P), ch = (n + P - 1) / P;
+    const uint32_t nr = r0 + ch <= n ? ch : n - r0;
+    defer_any |= !mfree && !every && round_flat_pays(nr, n, sizeof(T));
+  }
+  constexpr uint32_t kDefer = defer_rounds<T>();
+  const uint32_t nring = defer_any ? kDefer + 1 : 2;
 
   Multi<T> M;
   M.sh.resize(P);
@@ -164,13 +182,17 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
     ST_CHECK(hipSetDevice(d.dev));
     ST_CHECK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
     ST_CHECK(hipMalloc(&d.a, sizeof(T) * (size_t)d.nrows * n));
-    for (int i = 0; i < 2; i++)
+    for (uint32_t i = 0; i < nring; i++)
       ST_CHECK(hipMalloc(&d.s[i], sizeof(T) * (size_t)P * chunk));
     for (int i = 0; i < (mfree ? 2 : 1); i++)
       ST_CHECK(hipMalloc(&d.v[i], sizeof(T) * (size_t)P * chunk));
     ST_CHECK(hipMalloc(&d.state, sizeof(st_state)));
     if (!mfree && round_flat_pays(d.nrows, n, sizeof(T)))
       ST_CHECK(hipMalloc(&d.part, sizeof(T) * round_flat_scratch(d.nrows, n)));
+    d.defer = d.part != nullptr && !every;
+    if (d.defer)
+      for (uint32_t i = 0; i < nring; i++)
+        ST_CHECK(hipMalloc(&d.inv[i], sizeof(T) * (size_t)P * chunk));
     ST_CHECK(hipMemsetAsync(d.state, 0, sizeof(st_state), d.stream));
     if (gen_kind == 0) {
       ST_CHECK(hipMemcpyAsync(d.a, mat + (size_t)d.row0 * n,
@@ -218,6 +240,14 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   }
   if (gather(M, 0, chunk))
     return -1;
+  for (uint32_t p = 0; p < P; p++) { // 1 / s_0 for the deferred loop
+    Shard<T>& d = M.sh[p];
+    if (d.defer) {
+      ST_CHECK(hipSetDevice(d.dev));
+      if (launch_recip<T>(d.s[0], d.inv[0], n, d.stream))
+        return -1;
+    }
+  }
   for (uint32_t p = 0; p < P; p++) { // the setup is not part of the loop time
     ST_CHECK(hipSetDevice(M.sh[p].dev));
     ST_CHECK(hipStreamSynchronize(M.sh[p].stream));
@@ -228,7 +258,7 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
       .count();
 
   const auto t1 = std::chrono::steady_clock::now();
-  uint32_t enqueued = 0, cur = 0, batch_no = 0;
+  uint32_t enqueued = 0, batch_no = 0;
   bool done = false;
   while (!done && enqueued < max_itr) {
     const uint32_t b = (max_itr - enqueued) < batch ? (max_itr - enqueued) : batch;
@@ -238,25 +268,40 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
         Shard<T>& d = M.sh[p];
         ST_CHECK(hipSetDevice(d.dev));
         int rc;
+        const uint32_t cur = k % nring, nxt = (k + 1) % nring;
         if (mfree)
-          rc = launch_mfree<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk,
+          rc = launch_mfree<T>(d.a, d.s[cur], d.s[nxt] + p * chunk,
                                d.v[k & 1], d.v[(k + 1) & 1], d.nrows, n,
                                d.row0, eps, k + 1, max_itr, sem, d.state,
                                d.stream);
-        else if (d.part)
-          rc = launch_round_flat<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk,
+        else if (d.defer) {
+          // stored: A_j, j = the last multiple of kDefer <= k (the block is
+          // private: no flush after the loop)
+          const uint32_t j0 = k - k % kDefer, np = k - j0;
+          const T* ps[kDefer];
+          const T* pi[kDefer];
+          for (uint32_t i = 0; i < np; i++) {
+            ps[i] = d.s[(j0 + i) % nring];
+            pi[i] = d.inv[(j0 + i) % nring];
+          }
+          rc = launch_round_flat_deferred<T>(
+            d.a, d.s[cur], d.inv[cur], d.s[nxt] + p * chunk,
+            d.inv[nxt] + d.row0, d.part, d.v[0], d.nrows, n, d.row0, eps, k,
+            max_itr, sem, d.state, ps, pi, np, np + 1 == kDefer, false,
+            d.stream);
+        } else if (d.part)
+          rc = launch_round_flat<T>(d.a, d.s[cur], d.s[nxt] + p * chunk,
                                     d.part, d.v[0], d.nrows, n, d.row0, eps, k,
                                     max_itr, sem, d.state, d.stream);
         else
-          rc = launch_round<T>(d.a, d.s[cur], d.s[cur ^ 1] + p * chunk, d.v[0],
+          rc = launch_round<T>(d.a, d.s[cur], d.s[nxt] + p * chunk, d.v[0],
                                d.nrows, n, d.row0, eps, k, max_itr, sem,
                                d.state, d.stream);
         if (rc)
           return -1;
       }
-      if (gather(M, cur ^ 1, chunk))
+      if (gather(M, (k + 1) % nring, chunk))
         return -1;
-      cur ^= 1;
     }
     enqueued += b;
     const int slot = batch_no & 1;

@@ -18,7 +18,8 @@ _GEN = {"host": 0, "hilbert": 1, "random": 2}
 def solve_multi(n: int, matrix: Union[str, np.ndarray] = "hilbert", *, ngpus: int = 1,
                 devices: Optional[Sequence[int]] = None, seed: int = 0, dtype=np.float64,
                 eps: Optional[float] = None, max_itr: int = 0,
-                semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False, batch: int = 0):
+                semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False, batch: int = 0,
+                write_every_round: bool = False):
     """Returns (λ, v: ndarray, iterations, stats).
 
     ``matrix`` is a host (n, n) array, or "hilbert" / "random" to generate
@@ -43,7 +44,8 @@ def solve_multi(n: int, matrix: Union[str, np.ndarray] = "hilbert", *, ngpus: in
     ev = np.zeros(1, dtype=dtype)
     v = np.zeros(n, dtype=dtype)
     it = ctypes.c_uint32()
-    flags = _lib.ST_FLAG_MATRIX_FREE if matrix_free else 0
+    flags = ((_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
+             | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0))
     opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics, batch, flags)
     stats = _lib.st_stats()
     rc = getattr(L, f"st_solve_multi_{sfx}")(ptr, n, ngpus, dev_arr, kind, seed,

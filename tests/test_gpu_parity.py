@@ -856,6 +856,12 @@ def test_native_multi_gpu_flat_round(solver):
     lam1, v1, it1, st1 = solver.solve(a, inplace=True)
     assert lam == lam1 and it == it1 and st["rounds"] == st1["rounds"]
     assert np.array_equal(v, to_np(v1))
+    # deferred writes (the default) against storing every round, converging
+    # and fixed-round solves
+    for kw in (dict(), dict(eps=0.0, max_itr=8)):
+        r1 = solve_multi(n, "random", ngpus=1, seed=3, **kw)
+        r2 = solve_multi(n, "random", ngpus=1, seed=3, write_every_round=True, **kw)
+        assert r1[0] == r2[0] and r1[2] == r2[2] and np.array_equal(r1[1], r2[1]), kw
     del a
     torch.cuda.empty_cache()
 
