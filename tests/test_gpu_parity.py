@@ -1006,7 +1006,8 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 # and re-applies the pending scalings) against storing every round:
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------
-@pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144)])
+@pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144),
+                                  (np.float64, 4353)])   # odd: element-wide access
 @pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
 def test_deferred_writes_bitwise(solver, dt, n, sem):
     assert dev.flat_round_pays(n, n, TD[dt])
