@@ -147,9 +147,13 @@ def _declare(L: ctypes.CDLL) -> None:
                                                              i32, P, P]
         getattr(L, f"st_round_flat_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, T, u32,
                                                        u32, u32, P, P]
+        getattr(L, f"st_round_flat_deferred_{sfx}").argtypes = [
+            P, P, P, P, P, P, P, u32, u32, u32, T, u32, u32, u32, P, P, u32, i32, i32, P, P]
+        getattr(L, f"st_recip_{sfx}").argtypes = [P, P, u32, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
                      "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round",
-                     "round_split", "round_split_flat", "round_flat"):
+                     "round_split", "round_split_flat", "round_flat", "round_flat_deferred",
+                     "recip"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
     L.st_round_flat_scratch.argtypes = [u32, u32]
     L.st_round_flat_scratch.restype = u64
@@ -157,6 +161,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_round_split_flat_scratch.restype = u64
     L.st_round_flat_pays.argtypes = [u32, u32, i32]
     L.st_round_flat_pays.restype = i32
+    L.st_defer_rounds.argtypes = [i32]
+    L.st_defer_rounds.restype = u32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32
     L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]

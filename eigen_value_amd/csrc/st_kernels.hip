@@ -1127,6 +1127,40 @@ st_state_reset(st_state* d_state, void* stream)
 ST_STEP_EXPORTS(float, f32)
 ST_STEP_EXPORTS(double, f64)
 
+#define ST_DEFER_EXPORTS(T, SFX)                                               \
+  int st_round_flat_deferred_##SFX(                                            \
+    T* d_mat, const T* d_s_cur, const T* d_inv_cur, T* d_s_next,               \
+    T* d_inv_next, T* d_part, T* d_v, unsigned int nrows, unsigned int ncols,  \
+    unsigned int row0, T eps, unsigned int k, unsigned int max_itr,            \
+    unsigned int semantics, const T* const* d_pend_s,                          \
+    const T* const* d_pend_inv, unsigned int npend, int store, int flush,      \
+    st_state* d_state, void* stream)                                           \
+  {                                                                            \
+    st::clear_error();                                                         \
+    if (npend > 0 && (!d_pend_s || !d_pend_inv)) {                             \
+      st::set_error("round_flat_deferred: null pending list");                \
+      return -1;                                                               \
+    }                                                                          \
+    return st::launch_round_flat_deferred<T>(                                  \
+      d_mat, d_s_cur, d_inv_cur, d_s_next, d_inv_next, d_part, d_v, nrows,     \
+      ncols, row0, eps, k, max_itr, semantics, d_state, d_pend_s, d_pend_inv,  \
+      npend, store != 0, flush != 0, ST_STREAM(stream));                       \
+  }                                                                            \
+  int st_recip_##SFX(const T* d_s, T* d_inv, unsigned int n, void* stream)     \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_recip<T>(d_s, d_inv, n, ST_STREAM(stream));              \
+  }
+
+ST_DEFER_EXPORTS(float, f32)
+ST_DEFER_EXPORTS(double, f64)
+
+unsigned int
+st_defer_rounds(int dtype)
+{
+  return dtype == 1 ? st::defer_rounds<double>() : st::defer_rounds<float>();
+}
+
 uint64_t
 st_round_flat_scratch(unsigned int nrows, unsigned int ncols)
 {

@@ -188,6 +188,55 @@ def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float 
         eps, k, max_itr, semantics, _ptr(state), _stream(mat.device)), "round_flat")
 
 
+def defer_rounds(dtype) -> int:
+    """Rounds per store of the deferred flat round (st_defer_rounds)."""
+    torch = _torch()
+    return int(_lib.load().st_defer_rounds(1 if dtype == torch.float64 else 0))
+
+
+def recip(s, inv) -> None:
+    """inv = 1 / s elementwise (st_recip), the reciprocals the deferred round
+    re-applies."""
+    _check_cuda(s, inv)
+    assert inv.numel() >= s.numel() and inv.dtype == s.dtype
+    _lib.check(getattr(_lib.load(), f"st_recip_{_sfx(s)}")(
+        _ptr(s), _ptr(inv), s.numel(), _stream(s.device)), "recip")
+
+
+def flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next, part, v, state,
+                        pend_s=(), pend_inv=(), *, store: bool, flush: bool = False,
+                        row0: int = 0, eps: float = 1e-3, k: int = 0,
+                        max_itr: int = _lib.ST_MAX_ITR,
+                        semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """Round k of the flat round with deferred writes
+    (st_round_flat_deferred): ``mat`` holds the last STORED matrix A_j,
+    ``pend_s`` / ``pend_inv`` the pending rounds' full row-sum vectors
+    s_j .. s_{k-1} and their reciprocals; A_{k+1} is stored when ``store``.
+    s_next / inv_next are the block's slots (as in flat_round).  ``flush``
+    (with ``store``) only stores A_{k+1}.  Bit-identical to flat_round on a
+    matrix stored every round."""
+    import ctypes
+    _check_cuda(mat, s_cur, inv_cur, part, v, state, *pend_s, *pend_inv)
+    assert len(pend_s) == len(pend_inv) < defer_rounds(mat.dtype)
+    assert mat.is_contiguous() and mat.dim() == 2
+    nrows, ncols = mat.shape
+    assert s_cur.numel() >= ncols and inv_cur.numel() >= ncols and v.numel() >= ncols
+    assert all(x.numel() >= ncols for x in (*pend_s, *pend_inv))
+    assert row0 + nrows <= ncols
+    assert part.numel() >= int(_lib.load().st_round_flat_scratch(nrows, ncols))
+    if not flush:
+        _check_cuda(s_next, inv_next)
+        assert s_next.numel() >= nrows and inv_next.numel() >= nrows
+    np_ = len(pend_s)
+    arr_s = (ctypes.c_void_p * max(1, np_))(*[_ptr(x) for x in pend_s])
+    arr_i = (ctypes.c_void_p * max(1, np_))(*[_ptr(x) for x in pend_inv])
+    _lib.check(getattr(_lib.load(), f"st_round_flat_deferred_{_sfx(mat)}")(
+        _ptr(mat), _ptr(s_cur), _ptr(inv_cur), None if flush else _ptr(s_next),
+        None if flush else _ptr(inv_next), _ptr(part), _ptr(v), nrows, ncols, row0, eps, k,
+        max_itr, semantics, arr_s, arr_i, np_, int(store), int(flush), _ptr(state),
+        _stream(mat.device)), "round_flat_deferred")
+
+
 SPAN_LOCAL = 1
 SPAN_REMOTE = 2
 

@@ -127,6 +127,27 @@ class HipShardOps:
                              col0=col0, col1=col1, eps=eps, k=k, max_itr=max_itr,
                              semantics=semantics)
 
+    # deferred writes (solve loop only; bit-identical to storing every round)
+    def can_defer(self, nrows, ncols, dtype):
+        return self.dev.flat_round_pays(nrows, ncols, dtype)
+
+    def defer_rounds(self, dtype):
+        return self.dev.defer_rounds(dtype)
+
+    def recip(self, s, inv):
+        self.dev.recip(s, inv)
+
+    def round_deferred(self, mat, s_cur, inv_cur, s_next, inv_next, v, pend_s, pend_inv,
+                       row0, eps, k, max_itr, semantics, state, store, flush=False):
+        nrows, ncols = mat.shape
+        key = (nrows, ncols, mat.dtype)
+        if self._part is None or self._part[0] != key:
+            self._part = (key, self.dev.flat_scratch(nrows, ncols, mat.dtype, self.device))
+        self.dev.flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next, self._part[1], v,
+                                     state, pend_s, pend_inv, store=store, flush=flush,
+                                     row0=row0, eps=eps, k=k, max_itr=max_itr,
+                                     semantics=semantics)
+
     def make_streams(self):
         """(communication stream, 's_k slot ready' event, 'gathered' event)."""
         torch = self.torch
@@ -197,7 +218,7 @@ class ShardedSimilarityTransform:
 
     def __init__(self, n: int, dtype=None, group=None, ops=None,
                  semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False,
-                 comm: str = "auto", overlap: bool = False):
+                 comm: str = "auto", overlap: bool = False, deferred_writes: bool = True):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
@@ -220,6 +241,12 @@ class ShardedSimilarityTransform:
         if overlap and matrix_free:
             raise ValueError("overlap applies to the transform form only")
         self.overlap = overlap
+        # solve(): the flat round stores the block every m-th round (the
+        # library's deferred writes, bit-identical); round() always stores
+        self.deferred_writes = (deferred_writes and not matrix_free and not overlap
+                                and hasattr(self.ops, "round_deferred")
+                                and self.ops.can_defer(p.nrows, n, self.dtype))
+        self._ring = None
         self.part_sums = self.ops.empty((p.chunk,), self.dtype) if overlap else None
         # device ops overlap on a second stream; the CPU test double runs
         # the same calls in program order
@@ -356,11 +383,63 @@ class ShardedSimilarityTransform:
         self.gather(self.v)
         return self.v[:self.n]
 
+    def _solve_deferred(self, eps: float, max_itr: int, batch: int):
+        """solve() with deferred writes (st_round_flat_deferred): the block is
+        stored every m-th round and the rounds in between re-apply the pending
+        scalings from the last stored block, with the gathered row sums of the
+        pending rounds kept in a ring of m + 1 vectors (and their reciprocals).
+        One all-gather per round as before; bit-identical results; a final
+        flush leaves the block as storing every round would."""
+        p = self.part
+        m = self.ops.defer_rounds(self.dtype)
+        R = m + 1
+        if self._ring is None:
+            self._ring = ([self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(R)],
+                          [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(R)])
+        rs, ri = self._ring
+        full = lambda x: x[:p.n]                         # noqa: E731
+        pend = lambda j0, n_: ([full(rs[(j0 + i) % R]) for i in range(n_)],  # noqa: E731
+                               [full(ri[(j0 + i) % R]) for i in range(n_)])
+        self.ops.reset_state(self.state)
+        self.ops.fill(self.v, 1.0)
+        self.ops.rowsum(self.mat, self._slot(rs[0]))
+        self.gather(rs[0])
+        self.ops.recip(full(rs[0]), full(ri[0]))
+        k = 0
+        while k < max_itr:
+            for _ in range(min(batch, max_itr - k)):
+                cur, nxt, j0 = k % R, (k + 1) % R, k - k % m
+                ps, pi = pend(j0, k - j0)
+                self.ops.round_deferred(self.mat, full(rs[cur]), full(ri[cur]),
+                                        self._slot(rs[nxt]),
+                                        ri[nxt][p.row0:p.row0 + p.nrows], self.v, ps, pi,
+                                        p.row0, eps, k, max_itr, self.semantics, self.state,
+                                        store=(k - j0 + 1 == m))
+                self.gather(rs[nxt])
+                k += 1
+            if self.ops.read_state(self.state)["done"]:
+                break
+        st = self.ops.read_state(self.state)
+        if not st["done"]:
+            raise _lib.EigenValueError("sharded solve ended without done flag")
+        end = st["end"]
+        if end % m:
+            kl = end - 1
+            j0 = kl - kl % m
+            ps, pi = pend(j0, kl - j0)
+            self.ops.round_deferred(self.mat, full(rs[kl % R]), full(ri[kl % R]), None, None,
+                                    self.v, ps, pi, p.row0, eps, kl, max_itr, self.semantics,
+                                    self.state, store=True, flush=True)
+        self.k = end
+        return st["eigen_val"], self.eigen_vector(end), st["iters"], end
+
     def solve(self, eps: Optional[float] = None, max_itr: int = _lib.ST_MAX_ITR,
               batch: int = 4):
         """Run to convergence; returns (λ, v, iterations, rounds_evaluated)."""
         if eps is None:
             eps = 1e-3
+        if self.deferred_writes:
+            return self._solve_deferred(eps, max_itr, batch)
         self.start()
         while self.k < max_itr:
             b = min(batch, max_itr - self.k)

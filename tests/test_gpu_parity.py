@@ -365,6 +365,22 @@ def test_sharded_single_gpu_matches_device_solver(solver, n):
     assert torch.equal(v, v2)
 
 
+@pytest.mark.parametrize("kw", [dict(eps=1e-3), dict(eps=0.0, max_itr=7), dict(eps=0.0, max_itr=9)])
+def test_sharded_deferred_writes_bitwise(kw):
+    """The sharded driver's solve with deferred writes (the default on flat
+    blocks) == storing every round: λ, v, iterations and the final block."""
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+    out = []
+    for dw in (True, False):
+        sh = ShardedSimilarityTransform(4352, torch.float64, deferred_writes=dw)
+        assert sh.deferred_writes == dw
+        mat = sh.load("random", seed=8)
+        out.append((*sh.solve(**kw), mat.clone()))
+        sh.close()
+    (l0, v0, i0, r0, m0), (l1, v1, i1, r1, m1) = out
+    assert l0 == l1 and i0 == i1 and r0 == r1 and torch.equal(v0, v1) and torch.equal(m0, m1)
+
+
 def _gpu_gloo_worker(rank, world, port, n, outdir, overlap=False):
     import torch.distributed as dist
     from eigen_value_amd.sharded import ShardedSimilarityTransform
