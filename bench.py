@@ -372,10 +372,12 @@ def main():
     if world == 1 and not args.no_north_star:
         solver = dev.DeviceSolver(torch.device("cuda", dev_index))
         deferred = {}
-        for name, kind, nn, seed in (("configs[1] " + workload, args.kind, n, 0),
-                                     ("north_star random32768_f64", "random", 32768, 0)):
-            a0 = dev.generate(kind, nn, dt if nn == n else torch.float64, seed=seed,
-                              device=torch.device("cuda", dev_index))
+        for name, kind, nn, ddt in (("configs[1] " + workload, args.kind, n, dt),
+                                    ("north_star random32768_f64", "random", 32768,
+                                     torch.float64),
+                                    ("configs[4] random32768_f32", "random", 32768,
+                                     torch.float32)):
+            a0 = dev.generate(kind, nn, ddt, seed=0, device=torch.device("cuda", dev_index))
             if not dev.flat_round_pays(nn, nn, a0.dtype):
                 continue
             bpe = a0.element_size()
