@@ -400,7 +400,7 @@ def main():
                 per[every] = (t[40] - t[10]) / 30 * 1e3
             same = (res[False][0] == res[True][0] and torch.equal(res[False][1], res[True][1])
                     and (res[False][2] is None or torch.equal(res[False][2], res[True][2])))
-            every_m = 3 if bpe == 8 else 4          # defer_rounds<T>() in the library
+            every_m = dev.defer_rounds(nn, nn, a0.dtype)
             by = (every_m + 1.0) / every_m * nn * nn * bpe
             deferred[name] = {
                 "stores_every": every_m, "ms_per_iteration": round(per[False], 4),

@@ -161,7 +161,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_round_split_flat_scratch.restype = u64
     L.st_round_flat_pays.argtypes = [u32, u32, i32]
     L.st_round_flat_pays.restype = i32
-    L.st_defer_rounds.argtypes = [i32]
+    L.st_defer_rounds.argtypes = [u32, u32, i32]
     L.st_defer_rounds.restype = u32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32

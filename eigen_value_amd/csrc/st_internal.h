@@ -53,17 +53,13 @@ int launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
                       st_state* st, hipStream_t stream);
 size_t round_flat_scratch(uint32_t nrows, uint32_t ncols);
 bool round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem);
-// the flat round with deferred writes (A stored every defer_rounds<T>() rounds,
-// bit-identical results; FlatPending in st_device.h): npend pending rounds'
-// s and 1/s (oldest first), inv_cur = 1/s_cur, inv_next <- 1/s_{k+1};
+// the flat round with deferred writes (A stored every defer_rounds(...)
+// rounds, bit-identical results; FlatPending in st_device.h): npend pending
+// rounds' s and 1/s (oldest first), inv_cur = 1/s_cur, inv_next <- 1/s_{k+1};
 // flush = store the matrix only (after the loop; no row sums, no v)
-// rounds per store: 3 in fp64, 4 in fp32 (profiles/r01_sweep_defer_ring.log)
-template <typename T>
-constexpr uint32_t
-defer_rounds()
-{
-  return sizeof(T) == 8 ? 3u : 4u;
-}
+// rounds per store for a block: 4 on non-temporal blocks (>= 2 GiB), else 3
+// in fp64 and 4 in fp32 (profiles/r01_sweep_defer_rs.log)
+uint32_t defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem);
 constexpr uint32_t kDeferRoundsMax = 4;
 template <typename T>
 int launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur,

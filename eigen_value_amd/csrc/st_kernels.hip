@@ -530,7 +530,7 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 }
 
 // ---- the flat round with deferred writes ----------------------------------
-// (FlatPending in st_device.h): A is stored every defer_rounds<T>() rounds;
+// (FlatPending in st_device.h): A is stored every defer_rounds() rounds;
 // the rounds in between re-apply the pending scalings from
 // the last stored matrix, bit-identical to storing every round.
 // tools/sweep_dir.hip SWEEP_DEFER=1 [SWEEP_DEFER_RING=1],
@@ -540,7 +540,7 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 8192^2 fp64 0.125 vs 0.158; fp32 (every 4th, 4 rows) 0.821 vs 1.350 and
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
-template <typename T, int W, int ORDER, bool NT, int NP>
+template <typename T, int W, int ORDER, bool NT, int NP, int R>
 void
 launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         T* inv_next, T* part, T* v, uint32_t nrows,
@@ -549,7 +549,6 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         const T* const* pend_s, const T* const* pend_inv,
                         bool store, bool flush, hipStream_t stream)
 {
-  constexpr int R = sizeof(T) == 8 ? 2 : 4; // rows per workgroup
   const uint32_t ppr = flat_pieces(ncols, W);
   const uint32_t grid = (nrows + R - 1) / R * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
@@ -571,6 +570,10 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                        0u, 0u, 0u, inv_next);
 }
 
+// rows per workgroup of the deferred rounds (profiles/r01_sweep_defer_rs.log):
+// non-temporal blocks take 2 rows in the read-only rounds and 4 in the
+// storing round (whose pending scales are then loaded once for 4 rows);
+// cached blocks 2 (fp64) or 4 (fp32) throughout
 template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
@@ -581,19 +584,25 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
-#define ST_NP(NPV)                                                             \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV>(                               \
+  constexpr int RR = (sizeof(T) == 4 && !NT) ? 4 : 2; // read-only rounds
+  constexpr int RS = NT ? 4 : RR;                      // storing rounds
+#define ST_NP(NPV, RV)                                                         \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV>(                           \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, store, flush, stream)
-  switch (npend) {
-  case 0: ST_NP(0); break;
-  case 1: ST_NP(1); break;
-  case 2: ST_NP(2); break;
-  default:
-    if constexpr (defer_rounds<T>() > 3)
-      ST_NP(3);
-    break;
+#define ST_NP_R(RV)                                                            \
+  switch (npend) {                                                             \
+  case 0: ST_NP(0, RV); break;                                                 \
+  case 1: ST_NP(1, RV); break;                                                 \
+  case 2: ST_NP(2, RV); break;                                                 \
+  default: ST_NP(3, RV); break;                                                \
   }
+  if (store) {
+    ST_NP_R(RS)
+  } else {
+    ST_NP_R(RR)
+  }
+#undef ST_NP_R
 #undef ST_NP
 }
 
@@ -610,7 +619,7 @@ launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   ST_REQUIRE(a && s_cur && inv_cur && part && v && st,
              "round_flat_deferred: null pointer");
   ST_REQUIRE(flush || (s_next && inv_next), "round_flat_deferred: null pointer");
-  ST_REQUIRE(npend < defer_rounds<T>(),
+  ST_REQUIRE(npend < defer_rounds(nrows, ncols, sizeof(T)),
              "round_flat_deferred: %u pending rounds", npend);
   ST_REQUIRE(!flush || store, "round_flat_deferred: a flush stores");
   ST_REQUIRE(ncols > 0 && nrows > 0 && row0 + (uint64_t)nrows <= ncols,
@@ -640,6 +649,12 @@ launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
 #undef ST_DEF
   return check_launch("round_flat_deferred");
+}
+
+uint32_t
+defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem)
+{
+  return flat_round_nt(nrows, ncols, elem) ? 4u : (elem == 8 ? 3u : 4u);
 }
 
 template <typename T>
@@ -1156,9 +1171,9 @@ ST_DEFER_EXPORTS(float, f32)
 ST_DEFER_EXPORTS(double, f64)
 
 unsigned int
-st_defer_rounds(int dtype)
+st_defer_rounds(unsigned int nrows, unsigned int ncols, int dtype)
 {
-  return dtype == 1 ? st::defer_rounds<double>() : st::defer_rounds<float>();
+  return st::defer_rounds(nrows, ncols, dtype == 1 ? 8 : 4);
 }
 
 uint64_t

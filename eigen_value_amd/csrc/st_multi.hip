@@ -156,14 +156,14 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   ST_REQUIRE(sem <= ST_SEM_MAINPY, "unknown semantics %u", sem);
   // ring slots of the row-sum vectors: every shard gathers into the same
   // slot, so the ring is as long as the longest any shard needs
-  bool defer_any = false;
+  uint32_t nring = 2;
   for (uint32_t p = 0; p < P; p++) {
     const uint32_t r0 = p * ((n + P - 1) / P), ch = (n + P - 1) / P;
     const uint32_t nr = r0 + ch <= n ? ch : n - r0;
-    defer_any |= !mfree && !every && round_flat_pays(nr, n, sizeof(T));
+    if (!mfree && !every && round_flat_pays(nr, n, sizeof(T)) &&
+        defer_rounds(nr, n, sizeof(T)) + 1 > nring)
+      nring = defer_rounds(nr, n, sizeof(T)) + 1;
   }
-  constexpr uint32_t kDefer = defer_rounds<T>();
-  const uint32_t nring = defer_any ? kDefer + 1 : 2;
 
   Multi<T> M;
   M.sh.resize(P);
@@ -277,9 +277,10 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
         else if (d.defer) {
           // stored: A_j, j = the last multiple of kDefer <= k (the block is
           // private: no flush after the loop)
+          const uint32_t kDefer = defer_rounds(d.nrows, n, sizeof(T));
           const uint32_t j0 = k - k % kDefer, np = k - j0;
-          const T* ps[kDefer];
-          const T* pi[kDefer];
+          const T* ps[kDeferRoundsMax];
+          const T* pi[kDeferRoundsMax];
           for (uint32_t i = 0; i < np; i++) {
             ps[i] = d.s[(j0 + i) % nring];
             pi[i] = d.inv[(j0 + i) % nring];

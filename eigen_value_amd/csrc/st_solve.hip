@@ -208,10 +208,10 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   // the flat round stores the matrix every kDefer rounds (bit-identical
   // results; ST_FLAG_WRITE_EVERY_ROUND stores every round)
   const bool defer = flat && (o.flags & ST_FLAG_WRITE_EVERY_ROUND) == 0;
-  constexpr uint32_t kDefer = defer_rounds<T>();
-  constexpr uint32_t kR = kDefer + 1; // ring slots: pending + s_k + s_{k+1}
-  T* ring_s[kR];
-  T* ring_inv[kR];
+  const uint32_t kDefer = defer_rounds(n, n, sizeof(T));
+  const uint32_t kR = kDefer + 1; // ring slots: pending + s_k + s_{k+1}
+  T* ring_s[kDeferRoundsMax + 1];
+  T* ring_inv[kDeferRoundsMax + 1];
   for (uint32_t i = 0; i < kR; i++) {
     ring_s[i] = reinterpret_cast<T*>((char*)c->d_vec + (4 + i) * c->vec_bytes);
     ring_inv[i] = reinterpret_cast<T*>((char*)c->d_vec +
@@ -295,8 +295,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
       else if (defer) {
         // stored: A_j, j = the last multiple of kDefer <= k
         const uint32_t j0 = k - k % kDefer, np = k - j0;
-        const T* ps[kDefer];
-        const T* pi[kDefer];
+        const T* ps[kDeferRoundsMax];
+        const T* pi[kDeferRoundsMax];
         for (uint32_t i = 0; i < np; i++) {
           ps[i] = ring_s[(j0 + i) % kR];
           pi[i] = ring_inv[(j0 + i) % kR];
@@ -338,8 +338,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     // the matrix stands at A_J (J = the last store); apply rounds J .. end-1
     // and store A_end, exactly what storing every round leaves
     const uint32_t kl = fin.end - 1, j0 = kl - kl % kDefer, np = kl - j0;
-    const T* ps[kDefer];
-    const T* pi[kDefer];
+    const T* ps[kDeferRoundsMax];
+    const T* pi[kDeferRoundsMax];
     for (uint32_t i = 0; i < np; i++) {
       ps[i] = ring_s[(j0 + i) % kR];
       pi[i] = ring_inv[(j0 + i) % kR];

@@ -188,10 +188,12 @@ def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float 
         eps, k, max_itr, semantics, _ptr(state), _stream(mat.device)), "round_flat")
 
 
-def defer_rounds(dtype) -> int:
-    """Rounds per store of the deferred flat round (st_defer_rounds)."""
+def defer_rounds(nrows: int, ncols: int, dtype) -> int:
+    """Rounds per store of the deferred flat round on a block
+    (st_defer_rounds)."""
     torch = _torch()
-    return int(_lib.load().st_defer_rounds(1 if dtype == torch.float64 else 0))
+    return int(_lib.load().st_defer_rounds(nrows, ncols,
+                                           1 if dtype == torch.float64 else 0))
 
 
 def recip(s, inv) -> None:
@@ -217,7 +219,7 @@ def flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next, part, v, state,
     matrix stored every round."""
     import ctypes
     _check_cuda(mat, s_cur, inv_cur, part, v, state, *pend_s, *pend_inv)
-    assert len(pend_s) == len(pend_inv) < defer_rounds(mat.dtype)
+    assert len(pend_s) == len(pend_inv) < defer_rounds(*mat.shape, mat.dtype)
     assert mat.is_contiguous() and mat.dim() == 2
     nrows, ncols = mat.shape
     assert s_cur.numel() >= ncols and inv_cur.numel() >= ncols and v.numel() >= ncols

@@ -131,8 +131,8 @@ class HipShardOps:
     def can_defer(self, nrows, ncols, dtype):
         return self.dev.flat_round_pays(nrows, ncols, dtype)
 
-    def defer_rounds(self, dtype):
-        return self.dev.defer_rounds(dtype)
+    def defer_rounds(self, nrows, ncols, dtype):
+        return self.dev.defer_rounds(nrows, ncols, dtype)
 
     def recip(self, s, inv):
         self.dev.recip(s, inv)
@@ -391,7 +391,7 @@ class ShardedSimilarityTransform:
         One all-gather per round as before; bit-identical results; a final
         flush leaves the block as storing every round would."""
         p = self.part
-        m = self.ops.defer_rounds(self.dtype)
+        m = self.ops.defer_rounds(p.nrows, p.n, self.dtype)
         R = m + 1
         if self._ring is None:
             self._ring = ([self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(R)],

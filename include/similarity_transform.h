@@ -318,8 +318,8 @@ int st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype);
  * = 1 / d_s_cur; d_inv_next receives 1 / s_{k+1} for the block's rows (pass
  * the rank's slot, like d_s_next).  flush = 1 (with store = 1) only stores
  * A_{k+1} - no row sums, no v update - to leave the matrix as storing every
- * round would after the last round k.  npend < st_defer_rounds(dtype), the
- * rounds per store (3 fp64, 4 fp32).  d_pend_s / d_pend_inv are HOST arrays
+ * round would after the last round k.  npend < st_defer_rounds(nrows,
+ * ncols, dtype), the rounds per store.  d_pend_s / d_pend_inv are HOST arrays
  * of device pointers. */
 int st_round_flat_deferred_f32(float* d_mat, const float* d_s_cur,
                                const float* d_inv_cur, float* d_s_next,
@@ -346,8 +346,10 @@ int st_round_flat_deferred_f64(double* d_mat, const double* d_s_cur,
 int st_recip_f32(const float* d_s, float* d_inv, unsigned int n, void* stream);
 int st_recip_f64(const double* d_s, double* d_inv, unsigned int n,
                  void* stream);
-/* rounds per store of the deferred flat round (dtype 0 = f32, 1 = f64) */
-unsigned int st_defer_rounds(int dtype);
+/* rounds per store of the deferred flat round on a block (dtype 0 = f32,
+ * 1 = f64): 4 on blocks of >= 2 GiB, else 3 (f64) / 4 (f32) */
+unsigned int st_defer_rounds(unsigned int nrows, unsigned int ncols,
+                             int dtype);
 
 /* Round k split in two launches for a sharded solve that overlaps the
  * all-gather of s_k with compute (eigen_value_amd/sharded.py, overlap).

@@ -99,7 +99,8 @@ if __name__ == "__main__":
     p.add_argument("--write")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
-    m = 3 if a.dtype == "f64" else 4          # defer_rounds<T>() in the library
+    # rounds per store (st_defer_rounds): 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32
+    m = 4 if a.n * a.n * elem >= 2 << 30 else (3 if a.dtype == "f64" else 4)
     if a.trace or a.fetch:
         if a.trace:
             summarise(a.trace, a.n, elem, m)

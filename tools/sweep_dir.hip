@@ -279,10 +279,13 @@ defer_launch(const Bufs<T>& b, T* part, unsigned ppr, unsigned grid, int k,
                      ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pend);
 }
 
-template <typename T, bool NT, int MAXP, int R = 2, bool RING = false>
+template <typename T, bool NT, int MAXP, int R = 2, bool RING = false, int RS = R,
+          int R2 = R>
 static void
 defer_seq(const Bufs<T>& b, T* part)
 {
+  // RS: rows per workgroup of the storing round; R2: of the read-only rounds
+  // with 2 or more pending rounds (R for the others)
   // RING: s / 1/s in a ring of M + 1 distinct vectors as the solve loop
   // keeps them (otherwise every slot is the same vector)
   static_assert(MAXP <= 3, "pending rounds");
@@ -290,6 +293,8 @@ defer_seq(const Bufs<T>& b, T* part)
   constexpr int M = MAXP + 1;
   const unsigned ppr = (b.n + 256 * W - 1) / (256 * W);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
+  const unsigned grid_s = (b.nr + RS - 1) / RS * ppr;
+  const unsigned grid_2 = (b.nr + R2 - 1) / R2 * ppr;
   T* ring = nullptr;
   HIPCHECK(hipMalloc(&ring, sizeof(T) * (size_t)b.n * 2 * (M + 1)));
   for (int i = 0; i <= M; i++) {
@@ -311,11 +316,14 @@ defer_seq(const Bufs<T>& b, T* part)
       pi[i] = ri(j0 + i);
     }
     const bool store = np == M - 1;
-    switch (np) {
-    case 0: defer_launch<T, NT, R, 0>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
-    case 1: defer_launch<T, NT, R, 1>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
-    case 2: defer_launch<T, NT, R, 2>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
-    default: defer_launch<T, NT, R, 3>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, store); break;
+    if (store) {
+      defer_launch<T, NT, RS, MAXP>(b, part, ppr, grid_s, k, rs(k), ri(k), ps, pi, true);
+    } else {
+      switch (np) {
+      case 0: defer_launch<T, NT, R, 0>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, false); break;
+      case 1: defer_launch<T, NT, R, 1>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, false); break;
+      default: defer_launch<T, NT, R2, 2>(b, part, ppr, grid_2, k, rs(k), ri(k), ps, pi, false); break;
+      }
     }
     hipLaunchKernelGGL((k_parts<T>), dim3((b.nr + 3) / 4), dim3(256), 0, 0,
                        part, b.sn, b.nr, ppr, (uint32_t)k, b.st, rs(k), b.v, 0u,
@@ -323,9 +331,10 @@ defer_seq(const Bufs<T>& b, T* part)
   });
   HIPCHECK(hipFree(ring));
   const double bytes = (double)(M + 1) / M * b.nr * (double)b.n * sizeof(T);
-  std::printf("  defer m=%d r=%d ring=%d nt=%d  per round %8.4f ms  (%.3f N^2 b per round) "
-              "%7.1f GB/s\n",
-              M, R, (int)RING, (int)NT, t, (double)(M + 1) / M, bytes / (t * 1e-3) / 1e9);
+  std::printf("  defer m=%d r=%d r2=%d rs=%d ring=%d nt=%d  per round %8.4f ms  (%.3f N^2 b "
+              "per round) %7.1f GB/s\n",
+              M, R, R2, RS, (int)RING, (int)NT, t, (double)(M + 1) / M,
+              bytes / (t * 1e-3) / 1e9);
 }
 
 template <typename T>
@@ -423,6 +432,36 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_DEFER_RS")) { // rows of the storing round vs the others
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (int rep = 0; rep < 2; rep++) {
+      if (big) {
+        defer_seq<T, true, 2, 2, true, 2>(b, part);
+        defer_seq<T, true, 2, 2, true, 4>(b, part);
+        defer_seq<T, true, 3, 2, true, 4>(b, part);
+        defer_seq<T, true, 3, 2, true, 4, 4>(b, part);
+        defer_seq<T, true, 3, 2, true, 4, 1>(b, part);
+      } else {
+        defer_seq<T, false, 2, 2, true, 2>(b, part);
+        defer_seq<T, false, 2, 2, true, 4>(b, part);
+        defer_seq<T, false, 2, 2, true, 1>(b, part);
+        defer_seq<T, false, 3, 4, true, 4>(b, part);
+        defer_seq<T, false, 3, 4, true, 2>(b, part);
+        defer_seq<T, false, 3, 2, true, 4>(b, part);
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_DEFER")) { // deferred writes: store A every m rounds
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
