@@ -628,7 +628,7 @@ k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 }
 
 // ---------------------------------------------------------------------------
-// flat round, for blocks of 288 MiB and more (eigen_value_amd/csrc/
+// flat round, for blocks of 144 MiB and more (eigen_value_amd/csrc/
 // st_kernels.hip picks the form: cached accesses with ALT below 2 GiB,
 // non-temporal above)
 //

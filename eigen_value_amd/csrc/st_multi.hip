@@ -5,11 +5,11 @@
 // Device d owns rows [d*chunk, d*chunk + rows_d), chunk = ceil(N/P), and
 // keeps: its row block of A (transformed in place, or read only in the
 // matrix-free form), a ring of padded P*chunk row-sum vectors (two slots,
-// or defer_rounds + 1 when its block takes the flat round with deferred
+// or defer_rounds() + 1 when its block takes the flat round with deferred
 // writes, with their reciprocals), the eigenvector accumulator(s) and an
 // st_state.  Round k on every device:
-//   k_round / the flat round (deferred writes: A stored every 3rd fp64 /
-//   4th fp32 round, st_solve.hip) / k_mfree (launch k+1) on its stream
+//   k_round / the flat round (deferred writes: A stored every
+//   defer_rounds() rounds, st_solve.hip) / k_mfree (launch k+1) on its stream
 //   ncclAllGather(slot_d, s_next, chunk, type, comm_d, stream_d)
 // Every device derives m_k / stop_k from the identical gathered vector, so
 // the states agree without a further collective; the host polls device 0's
