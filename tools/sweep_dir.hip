@@ -280,10 +280,11 @@ defer_launch(const Bufs<T>& b, T* part, unsigned ppr, unsigned grid, int k,
 }
 
 template <typename T, bool NT, int MAXP, int R = 2, bool RING = false, int RS = R,
-          int R2 = R>
+          int R2 = R, bool RO = false>
 static void
 defer_seq(const Bufs<T>& b, T* part)
 {
+  // RO: never store (with MAXP = 0: a read-only flat pass every round)
   // RS: rows per workgroup of the storing round; R2: of the read-only rounds
   // with 2 or more pending rounds (R for the others)
   // RING: s / 1/s in a ring of M + 1 distinct vectors as the solve loop
@@ -315,9 +316,9 @@ defer_seq(const Bufs<T>& b, T* part)
       ps[i] = rs(j0 + i);
       pi[i] = ri(j0 + i);
     }
-    const bool store = np == M - 1;
-    if (store) {
-      defer_launch<T, NT, RS, MAXP>(b, part, ppr, grid_s, k, rs(k), ri(k), ps, pi, true);
+    const bool store = !RO && np == M - 1;
+    if (store || (RO && np == MAXP && MAXP > 2)) {
+      defer_launch<T, NT, RS, MAXP>(b, part, ppr, grid_s, k, rs(k), ri(k), ps, pi, store);
     } else {
       switch (np) {
       case 0: defer_launch<T, NT, R, 0>(b, part, ppr, grid, k, rs(k), ri(k), ps, pi, false); break;
@@ -432,6 +433,34 @@ run(unsigned nr, unsigned n)
   stream_seq<T, true>(b, true);
   stream_seq<T, false>(b, false);
   stream_seq<T, false>(b, true);
+  if (std::getenv("SWEEP_RO")) { // read-only flat passes vs k_mfree
+    T* part = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    for (int rep = 0; rep < 2; rep++) {
+      if (big) {
+        defer_seq<T, true, 0, 2, true, 2, 2, true>(b, part);
+        defer_seq<T, true, 0, 4, true, 4, 4, true>(b, part);
+      } else {
+        defer_seq<T, false, 0, 2, true, 2, 2, true>(b, part);
+        defer_seq<T, false, 0, 4, true, 4, 4, true>(b, part);
+      }
+      for (unsigned cap : { 512u }) {
+        mfree_seq<T, 4, true, false>(b, cap);
+        mfree_seq<T, 2, false, true>(b, cap);
+        mfree_seq<T, 4, false, true>(b, cap);
+      }
+    }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
   if (std::getenv("SWEEP_DEFER_RS")) { // rows of the storing round vs the others
     T* part = nullptr;
     const unsigned ppr = (b.n + 63) / 64;
