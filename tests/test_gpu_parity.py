@@ -823,6 +823,19 @@ def _rccl_worker(rank, port, outdir):
         sh.load("hilbert")
         lam, v, iters, rounds = sh.solve()
         np.save(os.path.join(outdir, "rccl.npy"), np.array([lam, iters, rounds]))
+        sh.close()
+        # a flat block: the deferred-write solve's ring of gathered row sums
+        # on the library communicator == storing every round
+        res = []
+        for dw in (True, False):
+            sh = ShardedSimilarityTransform(4352, torch.float64, deferred_writes=dw)
+            assert sh.deferred_writes == dw and sh.rccl is None   # P = 1: no comm needed
+            sh.load("random", seed=2)
+            res.append(sh.solve(eps=0.0, max_itr=10))
+            sh.close()
+        (l0, v0, i0, r0), (l1, v1, i1, r1) = res
+        np.save(os.path.join(outdir, "rccl_defer.npy"),
+                np.array([l0 == l1 and i0 == i1 and r0 == r1 and bool(torch.equal(v0, v1))]))
     finally:
         dist.destroy_process_group()
 
@@ -840,6 +853,7 @@ def test_rccl_process_group_single_rank(tmp_path, orc):
     ref = orc.similarity_transform(orc.hilbert(2048), orc.SEM_SYCL)
     assert int(iters) == ref.iter_count == 14
     assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert bool(np.load(tmp_path / "rccl_defer.npy")[0])
 
 
 @pytest.mark.parametrize("matrix_free", [False, True])
