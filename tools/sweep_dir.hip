@@ -570,10 +570,14 @@ run(unsigned nr, unsigned n)
 #define RB(R, FB)                                                              \
   (big ? flat2_seq<T, R, true, 2, FB, kGatePlain>(b, part)                     \
        : flat2_seq<T, R, false, 2, FB, kGatePlain>(b, part))
-    RB(1, 256); RB(2, 256); RB(4, 256);
-    RB(1, 128); RB(2, 128); RB(4, 128);
-    RB(1, 64);  RB(2, 64);  RB(4, 64);
-    RB(1, 512); RB(2, 512);
+    if (std::getenv("SWEEP_RB8")) {
+      RB(2, 256); RB(8, 64); RB(8, 128); RB(4, 64); RB(2, 256);
+    } else {
+      RB(1, 256); RB(2, 256); RB(4, 256);
+      RB(1, 128); RB(2, 128); RB(4, 128);
+      RB(1, 64);  RB(2, 64);  RB(4, 64);
+      RB(1, 512); RB(2, 512);
+    }
 #undef RB
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
