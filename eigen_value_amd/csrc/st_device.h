@@ -748,6 +748,24 @@ split_full_pieces(uint32_t ncols, uint32_t ppr, uint32_t col0, uint32_t col1,
   nfull = pb > pa ? pb - pa : 0u;
 }
 
+// k_flat's workgroup count (the launchers' grids): every row group over its
+// ppr pieces, or with SPLIT == 2 row group 0 over all of them and the rest
+// over the pieces not wholly inside [col0, col1)
+template <int R, uint32_t PWC, int SPLIT>
+__host__ __device__ inline uint32_t
+flat_nblocks(uint32_t nrows, uint32_t ncols, uint32_t ppr, uint32_t col0,
+             uint32_t col1)
+{
+  const uint32_t ng = (nrows + R - 1) / R;
+  if constexpr (SPLIT == 2) {
+    uint32_t pa, nfull;
+    split_full_pieces<PWC>(ncols, ppr, col0, col1, pa, nfull);
+    return ppr + (ng - 1) * (ppr - nfull);
+  } else {
+    return ng * ppr;
+  }
+}
+
 // How a flat workgroup learns that its launch follows the stopping round
 // (state->end != 0 && end <= k).  Millions of short workgroups each pay
 // this, so its latency matters (a persistent kernel pays it once per CU):
@@ -832,7 +850,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
-       FlatPending<T, NP> pend = FlatPending<T, NP>{})
+       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0)
 {
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
   // columns [col0, col1) whose scales this rank computed itself, over the
@@ -854,8 +872,21 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
   __shared__ T red[NW][R];
-  const uint32_t b = (ALT != 0 && (k & 1u)) ? flat_reverse<ALT>(blockIdx.x, gridDim.x)
-                                            : blockIdx.x;
+  // a dispatch counts at most 2^32 - 1 work-items per grid dimension, so a
+  // launch of more workgroups goes 2-D (gx2 = its row width, 0 = 1-D):
+  // fold blockIdx.y back in and drop the padding (uniform per workgroup;
+  // only huge matrices).  A kernel argument rather than gridDim.y, which
+  // would put a dispatch-packet load in front of every workgroup's loads.
+  uint32_t bl = blockIdx.x, nb;
+  if (gx2 != 0) {
+    bl += blockIdx.y * gx2;
+    nb = flat_nblocks<R, BLK * W, SPLIT>(nrows, ncols, ppr, col0, col1);
+    if (bl >= nb)
+      return;
+  } else {
+    nb = gridDim.x;
+  }
+  const uint32_t b = (ALT != 0 && (k & 1u)) ? flat_reverse<ALT>(bl, nb) : bl;
   uint32_t rg, p;                                  // p: index into this row's parts
   if constexpr (SPLIT == 2) {
     // the pieces wholly inside [col0, col1) have nothing to do past row

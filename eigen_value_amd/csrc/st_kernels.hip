@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "st_device.h"
 #include "st_internal.h"
 
@@ -44,7 +46,8 @@ check_launch(const char* what)
 // flight; the grid strides over the row groups.  What pays depends on the
 // size of the (local) matrix relative to the caches — 4 MB L2 per XCD, the
 // 256 MB memory-side cache (MALL) — so the shape is picked per launch:
-//   * matrices that outgrow the MALL (k_round >= 1 GiB, k_mfree >= 512 MiB)
+//   * matrices that outgrow the MALL (k_round >= 1 GiB, k_mfree >= 512 MiB,
+//     k_flat >= 2 GiB)
 //     use non-temporal loads/stores; below that, cached accesses let the
 //     MALL serve part of the next round;
 //   * every workgroup keeps the same row groups each round (same XCD, same
@@ -120,6 +123,33 @@ constexpr int kFlatAlt = 2;  // odd rounds: pieces reversed per XCD (flat_revers
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
 // than in a k_stats launch of their own (three)
 constexpr bool kFlatFusedStats = true;
+
+// A dispatch counts at most 2^32 - 1 work-items per grid dimension, so a
+// flat launch of more than kFlatGridX workgroups (fp64 from 131072^2, fp32
+// from ~185000^2) goes 2-D; k_flat folds blockIdx.y back in.  A multiple of
+// 8, so a workgroup's XCD (linear id % 8) stays the same.
+// st_set_flat_grid_limit lowers it (tests: the 2-D form at small sizes).
+constexpr uint32_t kFlatGridX = (0xffffffffu / kBlock) & ~7u;
+std::atomic<uint32_t> g_flat_grid_x{ kFlatGridX };
+
+struct FlatGrid
+{
+  dim3 grid;
+  uint32_t gx2; // k_flat's gx2 argument: the row width of a 2-D grid, else 0
+};
+
+inline FlatGrid
+flat_grid(uint32_t nb)
+{
+  const uint32_t gmax = g_flat_grid_x.load(std::memory_order_relaxed);
+  if (nb <= gmax)
+    return { dim3(nb), 0u };
+  // as few rows as fit, as narrow as they can be: < 8 padding workgroups
+  // per row (they exit at once)
+  const uint32_t gy = (nb + gmax - 1) / gmax;
+  const uint32_t gx = ((nb + gy - 1) / gy + 7u) & ~7u;
+  return { dim3(gx, gy), gx };
+}
 
 inline bool
 flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
@@ -463,13 +493,14 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
   const uint32_t ppr = flat_pieces(ncols, W);
   const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
+  const FlatGrid fg = flat_grid(grid);
   if constexpr (kFlatFusedStats) {
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt>), dim3(grid),
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt>), fg.grid,
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
-      st, eps, max_itr, semantics);
+      st, eps, max_itr, semantics, 0u, 0u, 0u, dev::FlatPending<T, -1>{}, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, s_cur, v, row0);
   } else {
@@ -479,8 +510,9 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
       (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt>),
-      dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols,
-      ppr, row0, k, st, eps, max_itr, semantics);
+      fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
+      row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u,
+      dev::FlatPending<T, -1>{}, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, nullptr, nullptr, 0u);
   }
@@ -559,11 +591,12 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
   pd.inv_cur = inv_cur;
   pd.store = store ? 1u : 0u;
+  const FlatGrid fg = flat_grid(grid);
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
                                   kBlock, 0, dev::kGatePlain, NP>),
-                     dim3(grid), dim3(kBlock), 0, stream, a, s_cur, part, v,
+                     fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
-                     0u, 0u, 0u, pd);
+                     0u, 0u, 0u, pd, fg.gx2);
   if (!flush) // a flush only stores the matrix: s, v and the state stand
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
@@ -721,32 +754,34 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
   if (span == 1) {
     if (npl == 0)
       return;
+    const FlatGrid fl = flat_grid(ngroups * npl);
     // a local half short of the whole row streams non-temporally at every
     // size: cached, it would evict from the MALL what the remote half is
     // about to re-read (profiles/r01_split_cost.log)
     if (NT || col1 - col0 < ncols)
       hipLaunchKernelGGL(
         (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
-        dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
-        nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
-        col1);
+        fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
+        npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
+        dev::FlatPending<T, -1>{}, fl.gx2);
     else
       hipLaunchKernelGGL(
         (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
-        dim3(ngroups * npl), dim3(kBlock), 0, stream, a, s_cur, part_local, v,
-        nrows, ncols, npl, row0, k, st, eps, max_itr, semantics, p_lo, col0,
-        col1);
+        fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
+        npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
+        dev::FlatPending<T, -1>{}, fl.gx2);
     return;
   }
   // row group 0 over every piece (it takes the stats), the other row
   // groups only over pieces holding remote columns
   uint32_t pa, nfull;
   dev::split_full_pieces<PW>(ncols, ppr, col0, col1, pa, nfull);
+  const FlatGrid fr = flat_grid(ppr + (ngroups - 1) * (ppr - nfull));
   hipLaunchKernelGGL(
     (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 2>),
-    dim3(ppr + (ngroups - 1) * (ppr - nfull)), dim3(kBlock), 0, stream, a,
-    s_cur, part, v, nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
-    0u, col0, col1);
+    fr.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
+    row0, k, st, eps, max_itr, semantics, 0u, col0, col1,
+    dev::FlatPending<T, -1>{}, fr.gx2);
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                      part, s_next, nrows, ppr, k, st, s_cur, v, row0,
@@ -1195,6 +1230,15 @@ int
 st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype)
 {
   return st::round_flat_pays(nrows, ncols, dtype == 1 ? 8 : 4) ? 1 : 0;
+}
+
+unsigned int
+st_set_flat_grid_limit(unsigned int max_x)
+{
+  const uint32_t gx = (max_x == 0 || max_x > st::kFlatGridX) ? st::kFlatGridX
+                      : (max_x < 8u ? 8u : (max_x & ~7u));
+  st::g_flat_grid_x.store(gx, std::memory_order_relaxed);
+  return gx;
 }
 
 } // extern "C"

@@ -7,8 +7,10 @@
 //
 // Round loop (one device stream, no per-round host sync):
 //   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
-//   per round k, ONE launch (k_round, st_device.h; matrices of >= 1 GiB
-//   take the flat round, k_flat + k_parts, instead):
+//   per round k, ONE launch (k_round, st_device.h; matrices of >= 144 MiB
+//   take the flat round, k_flat + k_parts, instead, storing the matrix
+//   every defer_rounds() rounds; N <= 128 fp64 / 256 fp32 run the whole
+//   loop in one k_solve_small launch):
 //     from s_k: max, v *= s/m, stop test, lambda = s_k[0] (every workgroup
 //     derives m_k/stop_k from its own sweep of s_k; workgroup 0 records)
 //     A_{k+1} = D_k^-1 A_k D_k in place, s_{k+1} = rowsum(A_{k+1})

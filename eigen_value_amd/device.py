@@ -188,6 +188,13 @@ def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float 
         eps, k, max_itr, semantics, _ptr(state), _stream(mat.device)), "round_flat")
 
 
+def set_flat_grid_limit(max_x: int = 0) -> int:
+    """Testing hook (st_set_flat_grid_limit): the width past which the flat
+    launches go 2-D (0 = the default, the dispatch limit).  Returns the
+    limit in force."""
+    return int(_lib.load().st_set_flat_grid_limit(max_x))
+
+
 def defer_rounds(nrows: int, ncols: int, dtype) -> int:
     """Rounds per store of the deferred flat round on a block
     (st_defer_rounds)."""

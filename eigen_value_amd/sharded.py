@@ -96,7 +96,7 @@ class HipShardOps:
         self.dev.epilogue(s, v, state, eps, max_itr, semantics)
 
     def round(self, mat, s_cur, s_next, v, row0, eps, k, max_itr, semantics, state):
-        # blocks of >= 1 GiB take the flat round (st_round_flat), the rest the
+        # blocks of >= 144 MiB take the flat round (st_round_flat), the rest the
         # one-launch k_round
         nrows, ncols = mat.shape
         if self.dev.flat_round_pays(nrows, ncols, mat.dtype):

@@ -307,6 +307,14 @@ int st_round_flat_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                       unsigned int semantics, st_state* d_state, void* stream);
 uint64_t st_round_flat_scratch(unsigned int nrows, unsigned int ncols);
 int st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype);
+/* Testing hook: the flat launches (k_flat, one workgroup per piece) spread
+ * more workgroups than a dispatch's 2^32 - 1 work-items per dimension allow
+ * (fp64 from 131072^2) over a 2-D grid of rows at most max_x wide; this lowers
+ * max_x (rounded down to a multiple of 8, at least 8; 0 restores the
+ * default, 16777208) so the 2-D form can be checked at small sizes.
+ * Process-wide; returns the limit now in force.  Results do not depend on
+ * it. */
+unsigned int st_set_flat_grid_limit(unsigned int max_x);
 
 /* Round k of the flat round with deferred writes (what the solve loops run
  * for blocks where st_round_flat_pays): the matrix in d_mat is the last

@@ -1055,6 +1055,69 @@ def test_deferred_writes_bitwise(solver, dt, n, sem):
         assert torch.equal(a1, a2), kw                      # final matrix bitwise
 
 
+@pytest.mark.parametrize("limit", [8, 1000, 4096])
+def test_flat_2d_grid_bitwise(solver, orc, limit):
+    """A flat launch of more workgroups than one dispatch dimension holds
+    (2^32 - 1 work-items: fp64 from 131072², test_max_single_gpu_size) goes
+    2-D.  Forced 2-D at small sizes (st_set_flat_grid_limit; widths that
+    divide the grid and ones that leave padding workgroups) every launch
+    form - the every-round and deferred solves, the two split halves - is
+    bit-identical to the 1-D grid."""
+    n = 4352                                                  # 144.5 MiB: flat
+    base = dev.generate("random", n, torch.float64, seed=6, device=DEV)
+    a = orc.random_matrix(6000, 3, np.float64, nrows=2049)    # split block
+    s_full = torch.from_numpy(orc.random_matrix(6000, 9, np.float64, nrows=1)[0] + 0.5).to(DEV)
+
+    def run():
+        out = []
+        for every in (False, True):
+            m = base.clone()
+            r = solver.solve(m, inplace=True, eps=0.0, max_itr=5, write_every_round=every)
+            out += [r[0], r[2], r[1].cpu(), m]
+        ta, tv = torch.from_numpy(a).to(DEV), torch.ones(6000, dtype=torch.float64, device=DEV)
+        s_next = torch.empty(2049, dtype=torch.float64, device=DEV)
+        part = dev.split_flat_scratch(2049, 6000, 3000, 5049, torch.float64, DEV)
+        state = dev.new_state(DEV)
+        for span in (dev.SPAN_LOCAL, dev.SPAN_REMOTE):
+            dev.split_flat_round(ta, s_full, s_next if span == dev.SPAN_REMOTE else None,
+                                 part, tv if span == dev.SPAN_REMOTE else None, state,
+                                 span=span, row0=3000, col0=3000, col1=5049, eps=1e-3, k=1)
+        return out + [ta, s_next, tv, dev.read_state(state)]
+
+    ref = run()
+    try:
+        assert dev.set_flat_grid_limit(limit) == limit
+        got = run()
+    finally:
+        assert dev.set_flat_grid_limit(0) == 16777208
+    for x, y in zip(ref, got):
+        assert (torch.equal(x, y) if isinstance(x, torch.Tensor) else x == y)
+
+
+def test_max_single_gpu_size(solver):
+    """131072² fp64 = 128 GiB on one GPU: the flat launches' 2^24 workgroups
+    exceed one dispatch dimension (2-D grid).  The deferred and every-round
+    transforms agree bit for bit, the matrix-free form to rounding, and λ
+    lies between the smallest and largest row sum (Perron-Frobenius)."""
+    n = 131072
+    torch.cuda.empty_cache()
+    a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    rs = a.sum(dim=1)
+    lo, hi = rs.min().item(), rs.max().item()
+    del rs
+    lam_mf, v_mf, it_mf, _ = solver.solve(a, matrix_free=True)
+    lam, v, it, st = solver.solve(a, inplace=True)                       # deferred
+    assert lo <= lam <= hi and it == it_mf and it >= 2
+    assert abs(lam - lam_mf) <= 1e-12 * lam and (v - v_mf).abs().max().item() <= 1e-12
+    dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
+    lam2, v2, it2, _ = solver.solve(a, inplace=True, write_every_round=True)
+    assert (lam2, it2) == (lam, it) and torch.equal(v2, v)
+    print(f"131072^2 f64: lambda {lam!r} in [{lo}, {hi}], {it} rounds, "
+          f"loop {st['loop_ms']:.1f} ms")
+    del a
+    torch.cuda.empty_cache()
+
+
 def test_deferred_writes_dropin_and_batches(eigen, orc):
     # the host-matrix path (private copy, no final flush) and batch sizes
     # that stop mid-group: identical to storing every round
