@@ -1037,15 +1037,18 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144),
-                                  (np.float64, 4353)])   # odd: element-wide access
+                                  (np.float64, 4353),    # odd: element-wide access
+                                  # just past 2 GiB: non-temporal, 4 rounds per
+                                  # store, element-wide (n % 16 B != 0)
+                                  (np.float64, 16385), (np.float32, 23171)])
 @pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
 def test_deferred_writes_bitwise(solver, dt, n, sem):
     assert dev.flat_round_pays(n, n, TD[dt])
     base = dev.generate("random", n, TD[dt], seed=4, device=DEV)
-    # fixed round counts ending at every residue mod 3 (the final flush), a
-    # converging solve, and max_itr = 1
+    # fixed round counts ending at every residue mod 3 and mod 4 (the final
+    # flush), a converging solve, and max_itr = 1
     for kw in (dict(eps=0.0, max_itr=7), dict(eps=0.0, max_itr=8), dict(eps=0.0, max_itr=9),
-               dict(), dict(eps=1e-9), dict(max_itr=1)):
+               dict(eps=0.0, max_itr=10), dict(), dict(eps=1e-9), dict(max_itr=1)):
         a1, a2 = base.clone(), base.clone()
         r1 = solver.solve(a1, inplace=True, semantics=sem, **kw)
         r2 = solver.solve(a2, inplace=True, semantics=sem, write_every_round=True, **kw)
