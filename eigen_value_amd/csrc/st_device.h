@@ -843,7 +843,7 @@ struct FlatPending
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain, int NP = -1>
+          int GATE = kGatePlain, int NP = -1, int U = 1>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -865,12 +865,17 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // R rows of one column piece per workgroup (the piece's column scales are
   // loaded once for the R rows); PW: one partial per wave instead of a
   // workgroup combine (no barrier before the workgroup retires)
+  // U: chunks of BLK * W columns per piece, chunk u of a lane BLK * W
+  // columns after chunk u - 1 (the element-wide path, W = 1, takes U =
+  // 16 / sizeof(T) so that its pieces hold as many bytes as the vector
+  // path's)
   if constexpr (GATE != kGateSpec) {
     if (flat_gated<GATE>(state, k))
       return;
   }
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
+  constexpr uint32_t PWC = (uint32_t)BLK * W * U; // columns per piece
   __shared__ T red[NW][R];
   // a dispatch counts at most 2^32 - 1 work-items per grid dimension, so a
   // launch of more workgroups goes 2-D (gx2 = its row width, 0 = 1-D):
@@ -880,7 +885,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   uint32_t bl = blockIdx.x, nb;
   if (gx2 != 0) {
     bl += blockIdx.y * gx2;
-    nb = flat_nblocks<R, BLK * W, SPLIT>(nrows, ncols, ppr, col0, col1);
+    nb = flat_nblocks<R, PWC, SPLIT>(nrows, ncols, ppr, col0, col1);
     if (bl >= nb)
       return;
   } else {
@@ -892,7 +897,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     // the pieces wholly inside [col0, col1) have nothing to do past row
     // group 0 (which takes the stats over every piece): the grid skips them
     uint32_t pa, nfull;
-    split_full_pieces<BLK * W>(ncols, ppr, col0, col1, pa, nfull);
+    split_full_pieces<PWC>(ncols, ppr, col0, col1, pa, nfull);
     if (b < ppr) {
       rg = 0;
       p = b;
@@ -906,36 +911,48 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     rg = b / ppr;
     p = b - rg * ppr;
   }
-  const uint32_t c = ((SPLIT == 1 ? p_lo + p : p) * BLK + threadIdx.x) * W;
+  const uint32_t c0 = ((SPLIT == 1 ? p_lo + p : p) * (uint32_t)(BLK * U) + threadIdx.x) * W;
   const uint32_t r0 = rg * R;
   T acc[R];
-  V x[R];
+  V x[U][R];
   T sr[R];
-  const bool in_cols = c < ncols; // ncols % W == 0 on the vector path
-  const bool in = in_cols && (SPLIT == 0 || ((c >= col0 && c < col1) == (SPLIT == 1)));
+  bool in_cols[U], in[U]; // ncols % W == 0 on the vector path
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const uint32_t c = c0 + u * BLK * W;
+    in_cols[u] = c < ncols;
+    in[u] = in_cols[u] && (SPLIT == 0 || ((c >= col0 && c < col1) == (SPLIT == 1)));
+  }
 #pragma unroll
   for (int j = 0; j < R; j++) {
     acc[j] = (T)0;
-    if (in && r0 + j < nrows)
-      x[j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c));
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (in[u] && r0 + j < nrows)
+        x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
+                                                 u * BLK * W));
     // s_k[r], or with deferred writes already 1 / s_k[r]
     const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
     sr[j] = r0 + j < nrows ? rs[row0 + r0 + j] : (T)1;
   }
   // the piece's column scales, issued with the matrix loads (the stats of
   // the first row group read them too)
-  V sc;
-  if (in_cols)
-    sc = *reinterpret_cast<const V*>(s_cur + c);
+  V sc[U];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    if (in_cols[u])
+      sc[u] = *reinterpret_cast<const V*>(s_cur + c0 + u * BLK * W);
   // deferred writes: the pending rounds' scales, issued with the matrix
   // loads
-  V sp_c[NP > 0 ? NP : 1];
+  V sp_c[NP > 0 ? NP : 1][U];
   T sp_r[NP > 0 ? NP : 1][R]; // 1 / s_i[r]
   if constexpr (NP > 0) {
 #pragma unroll
     for (int i = 0; i < NP; i++) {
-      if (in_cols)
-        sp_c[i] = *reinterpret_cast<const V*>(pend.s[i] + c);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (in_cols[u])
+          sp_c[i][u] = *reinterpret_cast<const V*>(pend.s[i] + c0 + u * BLK * W);
 #pragma unroll
       for (int j = 0; j < R; j++)
         sp_r[i][j] = r0 + j < nrows ? pend.inv[i][row0 + r0 + j] : (T)1;
@@ -950,9 +967,11 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       __shared__ T mx_sh[NW];
       T mx = (T)0;
       int ok = 1;
-      if (in_cols)
-        stats_at<T, W>(s_cur, sc, c / W, ncols, semantics == ST_SEM_SYCL, eps,
-                       mx, ok);
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (in_cols[u])
+          stats_at<T, W>(s_cur, sc[u], (c0 + u * BLK * W) / W, ncols,
+                         semantics == ST_SEM_SYCL, eps, mx, ok);
       int fail = ok ? 0 : 1;
       mx = wave_max(mx);
       if ((threadIdx.x & 63) == 0)
@@ -967,7 +986,10 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       }
     }
   }
-  if (in) {
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    if (!in[u])
+      continue;
     if constexpr (NP > 0) {
       // A_j -> A_k: the pending rounds' element updates, as they ran
 #pragma unroll
@@ -977,9 +999,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
           if (r0 + j < nrows) {
             const T inv = sp_r[i][j];
             if constexpr (ORDER == 0)
-              x[j] = x[j] * (inv * sp_c[i]);
+              x[u][j] = x[u][j] * (inv * sp_c[i][u]);
             else
-              x[j] = (inv * x[j]) * sp_c[i];
+              x[u][j] = (inv * x[u][j]) * sp_c[i][u];
           }
         }
       }
@@ -990,12 +1012,13 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
-          y = x[j] * (inv * sc); // cpp:324-325
+          y = x[u][j] * (inv * sc[u]); // cpp:324-325
         else
-          y = (inv * x[j]) * sc; // main.py:13-16
+          y = (inv * x[u][j]) * sc[u]; // main.py:13-16
         if (NP < 0 || pend.store)
-          st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c), y);
-        acc[j] = hsum<T, W>(y);
+          st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
+                    y);
+        acc[j] = u == 0 ? hsum<T, W>(y) : acc[j] + hsum<T, W>(y);
       }
     }
   }

@@ -163,6 +163,12 @@ flat_round_nt(uint32_t nrows, uint32_t ncols, size_t elem)
   return block_bytes(nrows, ncols, elem) >= ((size_t)2 << 30);
 }
 
+// chunks of kBlock * W columns per flat piece: the element-wide path
+// (W = 1) takes 16 / sizeof(T) of them, so that every piece holds 4 KB of
+// a row like the vector path's (profiles/r01_ragged_probe.log)
+template <typename T, int W>
+constexpr int kFlatU = W == 1 ? (int)(16 / sizeof(T)) : 1;
+
 // partial sums per row (one per piece) and the scratch they need
 inline uint32_t
 flat_pieces(uint32_t ncols, int w)
@@ -490,7 +496,8 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                   uint32_t k, uint32_t max_itr, uint32_t semantics,
                   st_state* st, hipStream_t stream)
 {
-  const uint32_t ppr = flat_pieces(ncols, W);
+  constexpr int U = kFlatU<T, W>;
+  const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   const FlatGrid fg = flat_grid(grid);
@@ -498,7 +505,9 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt>), fg.grid,
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 0,
+                   dev::kGatePlain, -1, U>),
+      fg.grid,
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
       st, eps, max_itr, semantics, 0u, 0u, 0u, dev::FlatPending<T, -1>{}, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
@@ -509,7 +518,8 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt>),
+      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt, kBlock, 0,
+                   dev::kGatePlain, -1, U>),
       fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
       row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u,
       dev::FlatPending<T, -1>{}, fg.gx2);
@@ -581,7 +591,8 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         const T* const* pend_s, const T* const* pend_inv,
                         bool store, bool flush, hipStream_t stream)
 {
-  const uint32_t ppr = flat_pieces(ncols, W);
+  constexpr int U = kFlatU<T, W>;
+  const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t grid = (nrows + R - 1) / R * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   dev::FlatPending<T, NP> pd{};
@@ -593,7 +604,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   pd.store = store ? 1u : 0u;
   const FlatGrid fg = flat_grid(grid);
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
-                                  kBlock, 0, dev::kGatePlain, NP>),
+                                  kBlock, 0, dev::kGatePlain, NP, U>),
                      fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
@@ -745,8 +756,9 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
                       uint32_t max_itr, uint32_t semantics, st_state* st,
                       hipStream_t stream)
 {
-  constexpr uint32_t PW = kBlock * W;
-  const uint32_t ppr = flat_pieces(ncols, W);
+  constexpr int U = kFlatU<T, W>;
+  constexpr uint32_t PW = kBlock * W * U;
+  const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t p_lo = col0 / PW;
   const uint32_t npl = col1 > col0 ? (col1 + PW - 1) / PW - p_lo : 0u;
   const uint32_t ngroups = (nrows + kFlatRows - 1) / kFlatRows;
@@ -760,13 +772,15 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
     // about to re-read (profiles/r01_split_cost.log)
     if (NT || col1 - col0 < ncols)
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
+        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, kFlatAlt, kBlock, 1,
+                     dev::kGatePlain, -1, U>),
         fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
         npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
         dev::FlatPending<T, -1>{}, fl.gx2);
     else
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, kFlatAlt, kBlock, 1>),
+        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, kFlatAlt, kBlock, 1,
+                     dev::kGatePlain, -1, U>),
         fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
         npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
         dev::FlatPending<T, -1>{}, fl.gx2);
@@ -778,7 +792,8 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
   dev::split_full_pieces<PW>(ncols, ppr, col0, col1, pa, nfull);
   const FlatGrid fr = flat_grid(ppr + (ngroups - 1) * (ppr - nfull));
   hipLaunchKernelGGL(
-    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 2>),
+    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 2,
+                 dev::kGatePlain, -1, U>),
     fr.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
     row0, k, st, eps, max_itr, semantics, 0u, col0, col1,
     dev::FlatPending<T, -1>{}, fr.gx2);
