@@ -193,6 +193,24 @@ st(V* p, const V& v)
 // buffer (ping-pong layout).  NT selects non-temporal (streaming) loads and
 // stores for the matrix.
 // ---------------------------------------------------------------------------
+// A lane's chunks [c, hi) (stride BLK) left after its full groups of U:
+// fewer than U, taken as groups of U/2, U/4, ..., 1 so that a group's loads
+// are in flight together (a one-chunk-at-a-time tail serialises up to U - 1
+// load latencies); column order, and so the sums, unchanged
+template <int U, int BLK, typename F>
+__device__ __forceinline__ void
+sweep_tail(uint32_t c, uint32_t hi, F&& body)
+{
+  if constexpr (U >= 2) {
+    constexpr int H = U / 2;
+    if (c + (H - 1) * BLK < hi) {
+      body(c, std::integral_constant<int, H>{});
+      c += H * BLK;
+    }
+    sweep_tail<H, BLK>(c, hi, body);
+  }
+}
+
 template <typename T, int ROWS, int W, int U, bool SCALE, bool SUM, int ORDER,
           bool NT, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
@@ -263,9 +281,7 @@ k_fused(const T* a_in, T* a_out, const T* __restrict__ s_cur,
     uint32_t c = threadIdx.x;
     for (; c + (U - 1) * BLK < nv; c += U * BLK)
       body(c, std::integral_constant<int, U>{});
-    if constexpr (U > 1)
-      for (; c < nv; c += BLK)
-        body(c, std::integral_constant<int, 1>{});
+    sweep_tail<U, BLK>(c, nv, body);
 
     if constexpr (SUM) {
       const int lane = threadIdx.x & 63;
@@ -414,9 +430,7 @@ round_group(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
     uint32_t c = lo + threadIdx.x;
     for (; c + (U - 1) * BLK < hi; c += U * BLK)
       body(c, std::integral_constant<int, U>{});
-    if constexpr (U > 1)
-      for (; c < hi; c += BLK)
-        body(c, std::integral_constant<int, 1>{});
+    sweep_tail<U, BLK>(c, hi, body);
   };
   if constexpr (SPAN == kSpanFull) {
     span(0, nv);
@@ -1228,9 +1242,7 @@ mfree_group(const T* a0, const T* __restrict__ s_prev,
   uint32_t c = threadIdx.x;
   for (; c + (U - 1) * BLK < nv; c += U * BLK)
     body(c, std::integral_constant<int, U>{});
-  if constexpr (U > 1)
-    for (; c < nv; c += BLK)
-      body(c, std::integral_constant<int, 1>{});
+  sweep_tail<U, BLK>(c, nv, body);
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;

@@ -65,6 +65,14 @@ constexpr int kRows = 2; // k_fused (K0 row sums and the step API)
 constexpr int kUnroll = 2;
 constexpr uint32_t kGridCap = 512;
 constexpr int kMfUnroll = 2;
+// the fp32 element-wide path (W = 1) keeps 4x the chunks in flight per
+// lane (as many bytes as the 16-byte vector path): 9-28 % faster k_mfree
+// and up to 3 % k_round on ragged fp32 sizes; fp64 is 1-7 % slower with
+// 2x, so it keeps kUnroll (a lane's columns are summed in column order
+// whatever the chunking, so results do not change;
+// profiles/r01_ragged_probe.log)
+template <typename T, int W, int U>
+constexpr int kChunks = (W == 1 && sizeof(T) == 4) ? 4 * U : U;
 
 struct Shape
 {
@@ -216,7 +224,7 @@ launch_rows(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
   const bool nt = fused_nt(nrows, ncols, sizeof(T));
   // small matrices: one row per workgroup keeps >= 256 workgroups busy
   if (nrows < 2 * kGridCap) {
-    launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(a, s_cur, s_next, 0, nrows,
+    launch_cfg<T, 1, W, kChunks<T, W, kUnroll>, SCALE, SUM, ORDER>(a, s_cur, s_next, 0, nrows,
                                                     ncols, row0, nt, st, stream);
     return;
   }
@@ -226,12 +234,12 @@ launch_rows(T* a, const T* s_cur, T* s_next, uint32_t nrows, uint32_t ncols,
   const int rows = nt ? R4 : kRows;
   const uint32_t full = nrows / rows;
   if (rows == 4)
-    launch_cfg<T, R4, W, kUnroll, SCALE, SUM, ORDER>(
+    launch_cfg<T, R4, W, kChunks<T, W, kUnroll>, SCALE, SUM, ORDER>(
       a, s_cur, s_next, 0, full, ncols, row0, nt, st, stream);
   else
-    launch_cfg<T, kRows, W, kUnroll, SCALE, SUM, ORDER>(
+    launch_cfg<T, kRows, W, kChunks<T, W, kUnroll>, SCALE, SUM, ORDER>(
       a, s_cur, s_next, 0, full, ncols, row0, nt, st, stream);
-  launch_cfg<T, 1, W, kUnroll, SCALE, SUM, ORDER>(
+  launch_cfg<T, 1, W, kChunks<T, W, kUnroll>, SCALE, SUM, ORDER>(
     a, s_cur, s_next, full * rows, nrows - full * rows, ncols, row0, nt, st,
     stream);
 }
@@ -263,7 +271,8 @@ launch_round_cfg(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
   const uint32_t ng = ng_main + nrem;
   const uint32_t grid = ng < cap ? ng : cap;
   hipLaunchKernelGGL(
-    (dev::k_round<T, ROWS, W, kUnroll, ORDER, NT, kBlock, true>), dim3(grid),
+    (dev::k_round<T, ROWS, W, kChunks<T, W, kUnroll>, ORDER, NT, kBlock, true>),
+    dim3(grid),
     dim3(kBlock), 0, stream, a, s_cur, s_next, v, ng_main, nrem, ncols, row0,
     eps, k, max_itr, semantics, st);
 }
@@ -302,7 +311,8 @@ launch_split_cfg(T* a, const T* s_cur, T* s_next, T* part, T* v,
   const uint32_t ng_main = nrows / ROWS, nrem = nrows % ROWS;
   const uint32_t ng = ng_main + nrem;
   const uint32_t grid = ng < cap ? ng : cap;
-  hipLaunchKernelGGL((dev::k_round_split<T, ROWS, W, kUnroll, ORDER, NT, SPAN>),
+  hipLaunchKernelGGL((dev::k_round_split<T, ROWS, W, kChunks<T, W, kUnroll>, ORDER, NT,
+                                          SPAN>),
                      dim3(grid), dim3(kBlock), 0, stream, a, s_cur, s_next,
                      part, v, ng_main, nrem, ncols, row0, q0, q1, eps, k,
                      max_itr, semantics, st);
@@ -365,7 +375,8 @@ launch_mfree_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
   const uint32_t ng = ng_main + nrem;
   const uint32_t grid = ng < cap ? ng : cap;
   hipLaunchKernelGGL(
-    (dev::k_mfree<T, ROWS, W, kMfUnroll, NT, kBlock, true>), dim3(grid),
+    (dev::k_mfree<T, ROWS, W, kChunks<T, W, kMfUnroll>, NT, kBlock, true>),
+    dim3(grid),
     dim3(kBlock), 0, stream, a0, s_prev, s_next, v_prev, v_cur, ng_main, nrem,
     ncols, row0, eps, k, max_itr, semantics, st);
 }
