@@ -45,7 +45,7 @@ def np_of(name):
     number of pending rounds it re-applies (its position in the group)."""
     import re
     m = re.search(r"k_flat<([^>]*)>", name)
-    return int(m.group(1).split(",")[-1])
+    return int(m.group(1).split(",")[11])
 
 
 def summarise(path, n, elem, m=3):

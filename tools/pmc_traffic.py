@@ -14,6 +14,9 @@ streaming read on gfx950, so the read side is doubled; WRITE_SIZE is exact
 for 16 B/lane streaming stores.  Launches that did no work (device-gated
 rounds after convergence) are dropped (< 10 % of the median traffic).
 The kernel trace gives the per-launch duration of the same command.
+Deferred-write launches of k_flat (template argument NP >= 0) are reported
+as k_flat_np<NP> against their own algorithmic bytes (N^2 b read-only,
+2 N^2 b for the storing launch); k_flat is the every-round transform.
 """
 import argparse
 import collections
@@ -22,24 +25,42 @@ import json
 import statistics
 
 
-def short(name):
+def flat_np(name):
+    """k_flat's NP template argument (the 12th): -1 = the every-round
+    transform, else the pending rounds a deferred-write launch re-applies."""
+    args = name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")
+    return int(args[11]) if len(args) > 11 else -1
+
+
+def flat_stores(name, m):
+    """Whether a deferred k_flat instance stores the matrix: the launch with
+    m - 1 pending rounds, and on non-temporal blocks every 4-row instance
+    (the launchers' storing shape, which the final flush also takes)."""
+    args = [x.strip() for x in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
+    return flat_np(name) == m - 1 or (args[3] == "true" and args[4] == "4")
+
+
+def short(name, m=3):
     base = name.split("(")[0].replace("void ", "")
-    return base.split("<")[0].split("::")[-1]
+    k = base.split("<")[0].split("::")[-1]
+    if k == "k_flat" and flat_np(name) >= 0:   # deferred writes (st_device.h FlatPending)
+        k = f"k_flat_np{flat_np(name)}" + ("_store" if flat_stores(name, m) else "")
+    return k
 
 
-def load_pmc(path):
+def load_pmc(path, m):
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        out[(short(r["Kernel_Name"]), r["Kernel_Name"].split("(")[0])].append(
+        out[(short(r["Kernel_Name"], m), r["Kernel_Name"].split("(")[0])].append(
             float(r["Counter_Value"]))
     return out
 
 
-def load_trace(path):
+def load_trace(path, m):
     out = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # ms
-        out[(short(r["Kernel_Name"]), r["Kernel_Name"].split("(")[0])].append(dur)
+        out[(short(r["Kernel_Name"], m), r["Kernel_Name"].split("(")[0])].append(dur)
     return out
 
 
@@ -54,10 +75,16 @@ def main():
     ap.add_argument("--trace")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
-    fetch, write = load_pmc(a.fetch), load_pmc(a.write)
-    trace = load_trace(a.trace) if a.trace else {}
-    algo = {"k_round": 2.0 * a.n * a.n * a.elem, "k_flat": 2.0 * a.n * a.n * a.elem,
-            "k_mfree": 1.0 * a.n * a.n * a.elem, "k_fused": 1.0 * a.n * a.n * a.elem}
+    nb = 1.0 * a.n * a.n * a.elem
+    # deferred writes: m rounds per store (st_defer_rounds); a storing
+    # launch moves 2 N^2 b, the others read N^2 b
+    m = 4 if nb >= 2 ** 31 else (3 if a.elem == 8 else 4)
+    fetch, write = load_pmc(a.fetch, m), load_pmc(a.write, m)
+    trace = load_trace(a.trace, m) if a.trace else {}
+    algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb}
+    for npend in range(m):
+        algo[f"k_flat_np{npend}"] = nb
+        algo[f"k_flat_np{npend}_store"] = 2.0 * nb
     entries = []
     for key in sorted(fetch):
         kname, full = key
@@ -87,7 +114,7 @@ def main():
            "fused_bytes_per_launch": fused[0]["hbm_bytes_per_launch"] if fused else None}
     json.dump(doc, open(a.out, "w"), indent=1)
     for e in entries:
-        print(f'{e["kernel"]:>8}: {e["hbm_bytes_per_launch"] / 1e9:8.3f} GB/launch '
+        print(f'{e["kernel"]:>17}: {e["hbm_bytes_per_launch"] / 1e9:8.3f} GB/launch '
               f'(algorithmic {e["algorithmic_bytes"] / 1e9:.3f}, x{e["traffic_over_algorithmic"]:.4f})'
               + (f', trace {e["trace_ms_avg"]:.4f} ms' if "trace_ms_avg" in e else ""))
 
