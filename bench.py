@@ -29,7 +29,8 @@ convergence: rounds, λ), `matrix_free` (the read-only form of the same
 iteration, SURVEY.md §8f item 1, priced against its own N^2*b bytes),
 `north_star` (32768x32768 random fp64, 1 GPU, both forms),
 `deferred_writes` (the library's solve loop, which stores the matrix every
-3rd fp64 / 4th fp32 round with bit-identical results, against storing every
+m-th round — 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32 (st_defer_rounds) —
+with bit-identical results, against storing every
 round; priced against its own (m+1)/m*N^2*b bytes) and, under
 `reference_headline`, `config0_hilbert128_gpu` (configs[0]'s 128^2 Hilbert
 solved on the GPU in one workgroup launch).
@@ -365,7 +366,8 @@ def main():
         torch.cuda.empty_cache()
 
     # ---- deferred writes: the library's solve loop (flat round, >= 144 MiB)
-    # stores A every 3rd round and re-applies the pending scalings in
+    # stores A every m-th round (st_defer_rounds) and re-applies the pending
+    # scalings in
     # registers, bit-identical to storing every round.  Per-round time from
     # the host clock of whole solves of 10 and 40 fixed rounds (eps = 0), the
     # difference over 30 rounds; the same with ST_FLAG_WRITE_EVERY_ROUND.

@@ -92,7 +92,8 @@ typedef struct st_options
                                 /* transform (input never written)         */
 #define ST_FLAG_WRITE_EVERY_ROUND 8u /* store the matrix every round; by    */
                                 /* default the flat round (>= 144 MiB)      */
-                                /* stores it every 3rd round and re-applies */
+                                /* stores it every 3rd/4th round (st_defer_ */
+                                /* rounds) and re-applies                   */
                                 /* the pending scalings in registers:       */
                                 /* identical results, fewer bytes           */
 #define ST_FLAG_ROUND_LOOP 4u   /* one launch per round even where the whole */

@@ -1032,7 +1032,7 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 
 
 # ---------------------------------------------------------------------------
-# deferred writes (blocks >= 144 MiB: the flat round stores A every 3rd round
+# deferred writes (blocks >= 144 MiB: the flat round stores A every 3rd/4th round
 # and re-applies the pending scalings) against storing every round:
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------
