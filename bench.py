@@ -367,8 +367,7 @@ def main():
 
     # ---- deferred writes: the library's solve loop (flat round, >= 144 MiB)
     # stores A every m-th round (st_defer_rounds) and re-applies the pending
-    # scalings in
-    # registers, bit-identical to storing every round.  Per-round time from
+    # scalings in registers, bit-identical to storing every round.  Per-round time from
     # the host clock of whole solves of 10 and 40 fixed rounds (eps = 0), the
     # difference over 30 rounds; the same with ST_FLAG_WRITE_EVERY_ROUND.
     if world == 1 and not args.no_north_star:
