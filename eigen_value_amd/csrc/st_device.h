@@ -662,8 +662,8 @@ k_round_split(T* a, const T* __restrict__ s_cur, T* __restrict__ s_next,
 //            wave per row), and v[r] *= s_k[r] / m_k      N * N/(BLK*W) * b
 // (k_stats is the same stats pass as a launch of its own: the three-launch
 // form, kept for the sweep tool.)  The row sums are deterministic and
-// independent of the row partition, but not bitwise k_round's (pieces are
-// summed apart).
+// independent of the row partition (for blocks of one piece size, kFlatU
+// in st_kernels.hip), but not bitwise k_round's (pieces are summed apart).
 // ---------------------------------------------------------------------------
 // thread 0 of each of `nwg` participating workgroups: fold the workgroup's
 // max (>= 0, not NaN) and failed-pair flag into st_state's scratch words;

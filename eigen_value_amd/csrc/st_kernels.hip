@@ -171,11 +171,16 @@ flat_round_nt(uint32_t nrows, uint32_t ncols, size_t elem)
   return block_bytes(nrows, ncols, elem) >= ((size_t)2 << 30);
 }
 
-// chunks of kBlock * W columns per flat piece: the element-wide path
-// (W = 1) takes 16 / sizeof(T) of them, so that every piece holds 4 KB of
-// a row like the vector path's (profiles/r01_ragged_probe.log)
-template <typename T, int W>
-constexpr int kFlatU = W == 1 ? (int)(16 / sizeof(T)) : 1;
+// chunks of kBlock * W columns per flat piece: 4 KB of a row per piece,
+// 8 KB for cached fp64 blocks (below 2 GiB: 1 % faster at 8192^2, 4-6 % on
+// the long-row P = 8 block 2880 x 23040; non-temporal blocks and fp32 lose
+// 1-7 %, profiles/r01_sweep_rbu.log); the element-wide path (W = 1) takes
+// 16 / sizeof(T) chunks so that its pieces hold as many bytes
+// (profiles/r01_ragged_probe.log).  Every flat launcher of a block takes
+// the same U, so the row sums' order is that of the block's pieces.
+template <typename T, int W, bool NT>
+constexpr int kFlatU =
+  (W == 1 ? (int)(16 / sizeof(T)) : 1) * ((sizeof(T) == 8 && !NT) ? 2 : 1);
 
 // partial sums per row (one per piece) and the scratch they need
 inline uint32_t
@@ -507,7 +512,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                   uint32_t k, uint32_t max_itr, uint32_t semantics,
                   st_state* st, hipStream_t stream)
 {
-  constexpr int U = kFlatU<T, W>;
+  constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
@@ -602,7 +607,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         const T* const* pend_s, const T* const* pend_inv,
                         bool store, bool flush, hipStream_t stream)
 {
-  constexpr int U = kFlatU<T, W>;
+  constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t grid = (nrows + R - 1) / R * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
@@ -767,7 +772,7 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
                       uint32_t max_itr, uint32_t semantics, st_state* st,
                       hipStream_t stream)
 {
-  constexpr int U = kFlatU<T, W>;
+  constexpr int U = kFlatU<T, W, NT>;
   constexpr uint32_t PW = kBlock * W * U;
   const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t p_lo = col0 / PW;

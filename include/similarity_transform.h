@@ -292,7 +292,9 @@ int st_round_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
  * full s_k; then the pieces' partial sums into s_next in a fixed order and
  * the eigenvector update.
  * Results as st_round_* except the row sums' summation order (deterministic
- * and independent of the row partition).  d_part: scratch of
+ * and independent of the row partition among blocks of one cache class:
+ * pieces are 8 KB of a row for fp64 blocks below 2 GiB, else 4 KB).
+ * d_part: scratch of
  * st_round_flat_scratch(nrows, ncols) elements.  st_round_flat_pays tells
  * whether this form is the faster one for a block (dtype 0 = f32, 1 = f64);
  * the library's own solve loops use it for such blocks. */

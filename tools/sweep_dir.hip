@@ -185,17 +185,18 @@ flat_seq(const Bufs<T>& b, T* part)
 // the two-launch flat round: stats folded into k_flat's first row group,
 // the v update into k_parts
 template <typename T, int R, bool NT = true, int ALT = 0, int FB = 256,
-          int GATE = kGateAtomic, int PT = 0>
+          int GATE = kGateAtomic, int PT = 0, int U = 1>
 static void
 flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
 {
   // lds: dynamic LDS reserved per workgroup (limits workgroups per CU)
   // PT: k_parts with one wave (0) or one thread (1) per row
+  // U: chunks of FB * W columns per piece
   constexpr int W = 16 / sizeof(T);
-  const unsigned ppr = (b.n + FB * W - 1) / (FB * W);
+  const unsigned ppr = (b.n + FB * W * U - 1) / (FB * W * U);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   float flat = time_seq([&](int k) {
-    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB, 0, GATE>),
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, FB, 0, GATE, -1, U>),
                        dim3(grid), dim3(FB), lds, 0, b.a, b.s, part, b.v, b.nr,
                        b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u);
     if constexpr (PT == 0)
@@ -207,9 +208,9 @@ flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
                          0u);
   });
   const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
-  std::printf("  flat2 r=%d nt=%d alt=%d blk=%d gate=%d lds=%5u pt=%d  round (2 launches) "
+  std::printf("  flat2 r=%d u=%d nt=%d alt=%d blk=%d gate=%d lds=%5u pt=%d  round (2 launches) "
               "%8.4f ms %7.1f GB/s\n",
-              R, (int)NT, (int)ALT, FB, GATE, lds, PT, flat, bytes / (flat * 1e-3) / 1e9);
+              R, U, (int)NT, (int)ALT, FB, GATE, lds, PT, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
 // k_round with the library's launch shape (round_shape in st_kernels.hip)
@@ -570,7 +571,12 @@ run(unsigned nr, unsigned n)
 #define RB(R, FB)                                                              \
   (big ? flat2_seq<T, R, true, 2, FB, kGatePlain>(b, part)                     \
        : flat2_seq<T, R, false, 2, FB, kGatePlain>(b, part))
-    if (std::getenv("SWEEP_RB8")) {
+#define RBU(R, U)                                                              \
+  (big ? flat2_seq<T, R, true, 2, 256, kGatePlain, 0, U>(b, part)              \
+       : flat2_seq<T, R, false, 2, 256, kGatePlain, 0, U>(b, part))
+    if (std::getenv("SWEEP_RBU")) { // chunks of 256 x 16 B per piece
+      RBU(2, 1); RBU(2, 2); RBU(1, 2); RBU(1, 4); RBU(2, 1); RBU(2, 2);
+    } else if (std::getenv("SWEEP_RB8")) {
       RB(2, 256); RB(8, 64); RB(8, 128); RB(4, 64); RB(2, 256);
     } else {
       RB(1, 256); RB(2, 256); RB(4, 256);
@@ -579,6 +585,7 @@ run(unsigned nr, unsigned n)
       RB(1, 512); RB(2, 512);
     }
 #undef RB
+#undef RBU
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
     HIPCHECK(hipFree(b.s));
