@@ -857,15 +857,20 @@ struct FlatPending
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain, int NP = -1, int U = 1>
+          int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
-       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0)
+       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0,
+       T* __restrict__ s_next = nullptr, uint32_t* __restrict__ fold_cnt = nullptr)
 {
+  // FOLD (sweep probe, SWEEP_FOLD=1 tools/sweep_dir): the last of a row
+  // group's ppr workgroups to finish sums the group's partials into s_next
+  // (k_parts' order, no v update) instead of a k_parts launch; fold_cnt[rg]
+  // counts arrivals and is reset by the last one
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
   // columns [col0, col1) whose scales this rank computed itself, over the
   // ppr pieces starting at piece p_lo (no stats, no v update); 2 = every
@@ -1060,7 +1065,43 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
       for (int w = 1; w < NW; w++)
         t += red[w][threadIdx.x];
-      part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+      if constexpr (FOLD) {
+        // an agent-scope atomic store (past the per-XCD L2s), completed
+        // before the arrival below (wave 0 waits on its memory counter)
+        __hip_atomic_store(&part[(size_t)(r0 + threadIdx.x) * ppr + p], t,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+      }
+    }
+    if constexpr (FOLD) {
+      if (wave == 0) {
+        // wave 0 wrote the partials: release them, count the arrival
+        uint32_t before = 0;
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane == 0) {
+          before = __hip_atomic_fetch_add(&fold_cnt[rg], 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        }
+        before = __shfl(before, 0);
+        if (before == ppr - 1) {
+#pragma unroll
+          for (int j = 0; j < R; j++) {
+            if (r0 + j < nrows) {
+              const T* row = part + (size_t)(r0 + j) * ppr;
+              T acc2 = (T)0;
+              for (uint32_t q = lane; q < ppr; q += 64)
+                acc2 += __hip_atomic_load(&row[q], __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+              acc2 = wave_sum(acc2);
+              if (lane == 0)
+                s_next[r0 + j] = acc2;
+            }
+          }
+          if (lane == 0)
+            fold_cnt[rg] = 0u;
+        }
+      }
     }
   }
 }

@@ -213,6 +213,26 @@ flat2_seq(const Bufs<T>& b, T* part, unsigned lds = 0)
               R, U, (int)NT, (int)ALT, FB, GATE, lds, PT, flat, bytes / (flat * 1e-3) / 1e9);
 }
 
+// the flat round with k_parts folded into k_flat (the last of a row group's
+// workgroups sums the group's partials; no v update): one launch per round
+template <typename T, int R, bool NT, int ALT, int U = 1>
+static void
+fold_seq(const Bufs<T>& b, T* part, uint32_t* cnt)
+{
+  constexpr int W = 16 / sizeof(T);
+  const unsigned ppr = (b.n + 256 * W * U - 1) / (256 * W * U);
+  const unsigned grid = (b.nr + R - 1) / R * ppr;
+  float t = time_seq([&](int k) {
+    hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, ALT, 256, 0, kGatePlain, -1, U, true>),
+                       dim3(grid), dim3(256), 0, 0, b.a, b.s, part, b.v, b.nr,
+                       b.n, ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u,
+                       FlatPending<T, -1>{}, 0u, b.sn, cnt);
+  });
+  const double bytes = 2.0 * b.nr * (double)b.n * sizeof(T);
+  std::printf("  fold  r=%d u=%d nt=%d alt=%d  round (1 launch) %8.4f ms %7.1f GB/s\n",
+              R, U, (int)NT, ALT, t, bytes / (t * 1e-3) / 1e9);
+}
+
 // k_round with the library's launch shape (round_shape in st_kernels.hip)
 template <typename T, int ROWS, int NT>
 static float
@@ -531,6 +551,37 @@ run(unsigned nr, unsigned n)
         }
       }
     }
+    HIPCHECK(hipFree(part));
+    HIPCHECK(hipFree(b.a));
+    HIPCHECK(hipFree(b.s));
+    HIPCHECK(hipFree(b.sn));
+    HIPCHECK(hipFree(b.v));
+    HIPCHECK(hipFree(b.v2));
+    HIPCHECK(hipFree(b.st));
+    return;
+  }
+  if (std::getenv("SWEEP_FOLD")) { // k_parts folded into k_flat (last arriver)
+    T* part = nullptr;
+    uint32_t* cnt = nullptr;
+    const unsigned ppr = (b.n + 63) / 64;
+    HIPCHECK(hipMalloc(&part, sizeof(T) * (size_t)b.nr * ppr * 4));
+    HIPCHECK(hipMalloc(&cnt, sizeof(uint32_t) * (size_t)b.nr));
+    HIPCHECK(hipMemset(cnt, 0, sizeof(uint32_t) * (size_t)b.nr));
+    const bool big = nn * sizeof(T) >= ((size_t)2 << 30);
+    const bool u2 = !big && sizeof(T) == 8;
+    for (int rep = 0; rep < 3; rep++) {
+      if (big) {
+        flat2_seq<T, 2, true, 0, 256, kGatePlain>(b, part);
+        fold_seq<T, 2, true, 0>(b, part, cnt);
+      } else if (u2) {
+        flat2_seq<T, 2, false, 2, 256, kGatePlain, 0, 2>(b, part);
+        fold_seq<T, 2, false, 2, 2>(b, part, cnt);
+      } else {
+        flat2_seq<T, 2, false, 2, 256, kGatePlain>(b, part);
+        fold_seq<T, 2, false, 2>(b, part, cnt);
+      }
+    }
+    HIPCHECK(hipFree(cnt));
     HIPCHECK(hipFree(part));
     HIPCHECK(hipFree(b.a));
     HIPCHECK(hipFree(b.s));
