@@ -74,6 +74,7 @@ assert ctypes.sizeof(st_options) == 24
 assert ctypes.sizeof(st_stats) == 56
 
 _lib: Optional[ctypes.CDLL] = None
+_by_path: dict = {}   # every library loaded, by real path (one CDLL each)
 
 
 def lib_path() -> str:
@@ -91,8 +92,12 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
             f"libsimilarity_transform.so not found at {p!r}: run `make` or "
             "`python -c 'import __graft_entry__ as g; g.build()'` first "
             "(there is no CPU fallback)")
-    L = ctypes.CDLL(p)
-    _declare(L)
+    key = os.path.realpath(p)
+    L = _by_path.get(key)
+    if L is None:
+        L = ctypes.CDLL(p)
+        _declare(L)
+        _by_path[key] = L
     if path is None:
         _lib = L
     return L
@@ -171,6 +176,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_comm_init.restype = i32
     L.st_comm_destroy.argtypes = [P]
     L.st_comm_destroy.restype = i32
+    L.st_comm_info.argtypes = [P, P, P, P]
+    L.st_comm_info.restype = i32
     for sfx in ("f32", "f64"):
         getattr(L, f"st_allgather_{sfx}").argtypes = [P, P, P, u64, P]
         getattr(L, f"st_allgather_{sfx}").restype = i32
@@ -178,14 +185,17 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_state_reset.restype = i32
 
 
-def last_error() -> str:
-    msg = load().eigen_last_error()
+def last_error(L: Optional[ctypes.CDLL] = None) -> str:
+    """The thread-local message of the library that made the failing call
+    (``L``; the default library when None)."""
+    msg = (L or load()).eigen_last_error()
     return msg.decode() if msg else ""
 
 
-def check(rc: int, what: str) -> int:
+def check(rc: int, what: str, L: Optional[ctypes.CDLL] = None) -> int:
+    """Raise EigenValueError for a negative return of a call into ``L``."""
     if rc < 0:
-        raise EigenValueError(f"{what} failed: {last_error() or 'unknown error'}")
+        raise EigenValueError(f"{what} failed: {last_error(L) or 'unknown error'}")
     return rc
 
 

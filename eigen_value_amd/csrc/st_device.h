@@ -322,8 +322,10 @@ k_fused(const T* a_in, T* a_out, const T* __restrict__ s_cur,
 // the round in `state`.  There is no separate epilogue launch.
 //
 // After the stop round the reference performs no more transforms; here the
-// stop round's launch still writes A_{k+1}/s_{k+1} (never observable: the
-// matrix is the solver's private copy, cpp:14,19) and every later launch
+// stop round's launch still writes A_{k+1}/s_{k+1} (lambda, v and the count
+// do not see it; the host-matrix solves work on a private copy, cpp:14,19,
+// and the device-resident solves document that d_mat ends at A_end) and
+// every later launch
 // returns at once: state->end = k+1 is set by the stop round, and launch j
 // exits if end != 0 && end <= j (a launch never gates on its own round).
 // ---------------------------------------------------------------------------

@@ -31,6 +31,26 @@ void clear_error();
     }                                                                          \
   } while (0)
 
+// Restores the caller's current HIP device when a C entry point returns
+// (by any path): contexts, shards and communicators switch devices
+// internally, and the caller's thread must not see that.
+struct DeviceGuard
+{
+  int prev = -1;
+  DeviceGuard()
+  {
+    if (hipGetDevice(&prev) != hipSuccess)
+      prev = -1;
+  }
+  ~DeviceGuard()
+  {
+    if (prev >= 0)
+      (void)hipSetDevice(prev);
+  }
+  DeviceGuard(const DeviceGuard&) = delete;
+  DeviceGuard& operator=(const DeviceGuard&) = delete;
+};
+
 // kernel launchers (st_kernels.hip); all asynchronous on `stream`
 template <typename T>
 int launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,

@@ -198,24 +198,23 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
       ST_CHECK(hipMemcpyAsync(d.a, mat + (size_t)d.row0 * n,
                               sizeof(T) * (size_t)d.nrows * n,
                               hipMemcpyHostToDevice, d.stream));
-    } else if (gen_kind == 1) {
-      if (sizeof(T) == 8)
-        ST_REQUIRE(st_generate_hilbert_f64((double*)d.a, d.nrows, n, d.row0,
-                                           d.stream) == 0,
-                   "%s", eigen_last_error());
-      else
-        ST_REQUIRE(st_generate_hilbert_f32((float*)d.a, d.nrows, n, d.row0,
-                                           d.stream) == 0,
-                   "%s", eigen_last_error());
     } else {
-      if (sizeof(T) == 8)
-        ST_REQUIRE(st_generate_random_f64((double*)d.a, d.nrows, n, d.row0,
-                                          seed, d.stream) == 0,
-                   "%s", eigen_last_error());
+      // the generators set the error message themselves on failure
+      int rc;
+      if (gen_kind == 1)
+        rc = sizeof(T) == 8
+               ? st_generate_hilbert_f64((double*)d.a, d.nrows, n, d.row0,
+                                         d.stream)
+               : st_generate_hilbert_f32((float*)d.a, d.nrows, n, d.row0,
+                                         d.stream);
       else
-        ST_REQUIRE(st_generate_random_f32((float*)d.a, d.nrows, n, d.row0,
-                                          seed, d.stream) == 0,
-                   "%s", eigen_last_error());
+        rc = sizeof(T) == 8
+               ? st_generate_random_f64((double*)d.a, d.nrows, n, d.row0,
+                                        seed, d.stream)
+               : st_generate_random_f32((float*)d.a, d.nrows, n, d.row0,
+                                        seed, d.stream);
+      if (rc != 0)
+        return -1;
     }
     if (launch_fill<T>(d.v[0], n, (T)1, d.stream)) // cpp:34
       return -1;
@@ -364,6 +363,7 @@ st_solve_multi_f32(const float* mat, unsigned int dim, int ngpus,
                    const st_options* opt, st_stats* stats)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_multi<float>(mat, dim, ngpus, devices, gen_kind, seed,
                                 eigen_val, eigen_vec, iter_cnt, opt, stats);
 }
@@ -376,6 +376,7 @@ st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
                    st_stats* stats)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_multi<double>(mat, dim, ngpus, devices, gen_kind, seed,
                                  eigen_val, eigen_vec, iter_cnt, opt, stats);
 }
@@ -401,6 +402,7 @@ int
 st_comm_init(void** comm, int nranks, int rank, const char* id_in, int device)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   ST_REQUIRE(comm && id_in, "st_comm_init: null pointer");
   ST_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "st_comm_init: bad rank");
   *comm = nullptr;
@@ -417,8 +419,24 @@ int
 st_comm_destroy(void* comm)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   if (comm)
     ST_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+  return 0;
+}
+
+int
+st_comm_info(void* comm, int* nranks, int* rank, int* device)
+{
+  st::clear_error();
+  ST_REQUIRE(comm, "st_comm_info: null communicator");
+  const ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+  if (nranks)
+    ST_NCCL(ncclCommCount(c, nranks));
+  if (rank)
+    ST_NCCL(ncclCommUserRank(c, rank));
+  if (device)
+    ST_NCCL(ncclCommCuDevice(c, device));
   return 0;
 }
 

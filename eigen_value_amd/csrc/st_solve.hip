@@ -466,6 +466,7 @@ void
 make_queue(void** wq)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   if (!wq)
     return;
   *wq = nullptr;
@@ -505,6 +506,7 @@ make_queue(void** wq)
 void
 destroy_queue(void* wq)
 {
+  st::DeviceGuard guard;
   Context* c = st::as_ctx(wq);
   if (!c)
     return;
@@ -569,6 +571,7 @@ max_eigen_value(void* wq, float* mat, float* eigen_val, float* eigen_vec,
                 unsigned int dim, unsigned int* iter_cnt)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_host<float>(st::as_ctx(wq), mat, dim, eigen_val, eigen_vec,
                                iter_cnt, nullptr, nullptr);
 }
@@ -579,6 +582,7 @@ max_eigen_value_f64(void* wq, double* mat, double* eigen_val,
                     unsigned int* iter_cnt)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_host<double>(st::as_ctx(wq), mat, dim, eigen_val,
                                 eigen_vec, iter_cnt, nullptr, nullptr);
 }
@@ -589,6 +593,7 @@ max_eigen_value_ex(void* wq, int dtype, const void* mat, void* eigen_val,
                    const st_options* opt, st_stats* stats)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   if (dtype == 0)
     return st::solve_host<float>(st::as_ctx(wq), (const float*)mat, dim,
                                  (float*)eigen_val, (float*)eigen_vec,
@@ -608,6 +613,7 @@ st_solve_device_f32(void* wq, float* d_mat, unsigned int dim,
                     const st_options* opt, st_stats* stats)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_device<float>(st::as_ctx(wq), d_mat, dim, d_eigen_vec,
                                  eigen_vec_host, eigen_val, iter_cnt, opt,
                                  stats);
@@ -620,6 +626,7 @@ st_solve_device_f64(void* wq, double* d_mat, unsigned int dim,
                     const st_options* opt, st_stats* stats)
 {
   st::clear_error();
+  st::DeviceGuard guard;
   return st::solve_device<double>(st::as_ctx(wq), d_mat, dim, d_eigen_vec,
                                   eigen_vec_host, eigen_val, iter_cnt, opt,
                                   stats);

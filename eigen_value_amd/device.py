@@ -333,11 +333,15 @@ class DeviceSolver:
         round instead (``ST_FLAG_ROUND_LOOP``).  Matrices of >= 144 MiB
         store the transformed matrix every 3rd or 4th round
         (``defer_rounds``) and re-apply the pending scalings in registers
-        (identical results and final matrix, a third to 3/8 fewer bytes); ``write_every_round`` stores it every round
+        (identical results and final matrix, a third to 3/8 fewer bytes);
+        ``write_every_round`` stores it every round
         (``ST_FLAG_WRITE_EVERY_ROUND``).
 
         ``mat`` is transformed in place when ``inplace`` (it is the private
-        working copy the reference makes, similarity_transform.cpp:14,19).
+        working copy the reference makes, similarity_transform.cpp:14,19)
+        and then ends at A_end, end = ``stats["rounds"]``: the stopping
+        round's launch still applies its transform, one more than the
+        reference loop, which breaks before compute_next_matrix (cpp:45-52).
         ``matrix_free`` runs the read-only form: the
         input is never written, so no copy is made.  ``mat`` may be a torch
         tensor or any DLPack producer (``__dlpack__``) on this device."""

@@ -190,6 +190,14 @@ class RcclComm:
                    "st_comm_init")
         self.rank, self.world = rank, world
 
+    def info(self) -> dict:
+        """What RCCL itself reports for this communicator (st_comm_info)."""
+        ctypes = self.ctypes
+        n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.L.st_comm_info(self.comm, ctypes.byref(n), ctypes.byref(r),
+                                       ctypes.byref(d)), "st_comm_info")
+        return {"nranks": n.value, "rank": r.value, "device": d.value}
+
     def allgather(self, out, inp) -> None:
         sfx = "f64" if out.dtype == self.torch.float64 else "f32"
         stream = self.torch.cuda.current_stream(out.device).cuda_stream

@@ -45,7 +45,7 @@ class EigenValue:
         self.sycl_q = ctypes.c_void_p()
         self.so_lib.make_queue(ctypes.byref(self.sycl_q))
         if self.sycl_q.value is None:
-            raise Exception(f'failed to get default HIP queue: {_lib.last_error()}')
+            raise Exception(f'failed to get default HIP queue: {_lib.last_error(self.so_lib)}')
 
     # ------------------------------------------------------------------
     def similarity_transform(self, mat: np.ndarray) -> Tuple[np.floating, np.ndarray, int, int]:
@@ -68,7 +68,7 @@ class EigenValue:
         fn = self.so_lib.max_eigen_value if mat.dtype == np.float32 else self.so_lib.max_eigen_value_f64
         ts = fn(self.sycl_q, mat.ctypes.data, eigen_val.ctypes.data,
                 eigen_vec.ctypes.data, n, iter_cnt.ctypes.data)
-        _lib.check(ts, "max_eigen_value")
+        _lib.check(ts, "max_eigen_value", self.so_lib)
         return eigen_val[0], eigen_vec, int(ts), int(iter_cnt[0])
 
     # ------------------------------------------------------------------
@@ -105,18 +105,18 @@ class EigenValue:
             self.sycl_q, dtype, mat.ctypes.data, eigen_val.ctypes.data,
             eigen_vec.ctypes.data, n, iter_cnt.ctypes.data,
             ctypes.byref(opt), ctypes.byref(stats))
-        _lib.check(ts, "max_eigen_value_ex")
+        _lib.check(ts, "max_eigen_value_ex", self.so_lib)
         return eigen_val[0], eigen_vec, int(ts), int(iter_cnt[0]), stats.as_dict()
 
     def last_round_times(self) -> np.ndarray:
         """Per-round kernel times (ms) of the last ``similarity_transform_ex``
         call made with ``time_kernels=True`` (empty otherwise)."""
-        n = _lib.check(self.so_lib.st_last_round_times(self.sycl_q, None, 0),
-                       "st_last_round_times")
+        L = self.so_lib
+        n = _lib.check(L.st_last_round_times(self.sycl_q, None, 0), "st_last_round_times", L)
         out = np.zeros(n, dtype=np.float32)
         if n:
-            _lib.check(self.so_lib.st_last_round_times(self.sycl_q, out.ctypes.data, n),
-                       "st_last_round_times")
+            _lib.check(L.st_last_round_times(self.sycl_q, out.ctypes.data, n),
+                       "st_last_round_times", L)
         return out
 
     # ------------------------------------------------------------------

@@ -139,7 +139,14 @@ int st_use_own_stream(void* wq);
 
 /* d_mat: device pointer, dim x dim row-major; TRANSFORMED IN PLACE (it is
  * the private working copy the reference makes at
- * similarity_transform.cpp:14,19).  d_eigen_vec: device pointer [dim] or
+ * similarity_transform.cpp:14,19).  On return d_mat holds A_end, where end =
+ * st_stats.rounds = the rounds evaluated: the launch that evaluates the
+ * stopping round still applies its transform, so a converged solve leaves
+ * one transform more than the reference's working copy, whose loop breaks
+ * before compute_next_matrix (similarity_transform.cpp:45-52); an
+ * exhausted solve (MAX_ITR rounds) leaves A_MAX_ITR like the reference.
+ * lambda, the eigenvector and iter_cnt do not depend on it.  d_eigen_vec:
+ * device pointer [dim] or
  * NULL (then eigen_vec_host must be non-NULL and receives it).
  * eigen_val / iter_cnt: host pointers.  Returns loop ms or negative. */
 int64_t st_solve_device_f32(void* wq, float* d_mat, unsigned int dim,
@@ -182,6 +189,10 @@ int st_comm_unique_id(char* id_out);
 int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
                  int device);
 int st_comm_destroy(void* comm);
+/* What the communicator itself reports (ncclCommCount / ncclCommUserRank /
+ * ncclCommCuDevice): the ranks RCCL joined, this rank, its HIP device.
+ * Any output pointer may be NULL.  Returns 0 or negative. */
+int st_comm_info(void* comm, int* nranks, int* rank, int* device);
 int st_allgather_f32(void* comm, const float* send, float* recv,
                      uint64_t count, void* stream);
 int st_allgather_f64(void* comm, const double* send, double* recv,

@@ -152,6 +152,83 @@ class CpuShardOps:
         return dict(st)
 
 
+class CpuDeferOps(CpuShardOps):
+    """CpuShardOps plus the deferred-write contract (st_round_flat_deferred,
+    include/similarity_transform.h), so the driver's _solve_deferred runs on
+    CPU: its ring of gathered row sums, the per-rank reciprocals (only the
+    own rows of 1/s are written), the final flush.  ``defer(nrows)`` decides
+    per block whether the rank defers and ``rounds(nrows)`` its rounds per
+    store, so ranks of one solve can disagree on both, as uneven row blocks
+    do on the GPU (the last block is smaller)."""
+
+    def __init__(self, defer=lambda nrows: True, rounds=lambda nrows: 3):
+        super().__init__()
+        self._defer, self._rounds = defer, rounds
+        self.stores = 0
+
+    def can_defer(self, nrows, ncols, dtype):
+        return bool(self._defer(nrows))
+
+    def defer_rounds(self, nrows, ncols, dtype):
+        return int(self._rounds(nrows))
+
+    def recip(self, s, inv):
+        inv[:s.numel()] = 1 / s
+
+    @staticmethod
+    def _update(a, inv_rows, s_cols, order):
+        # x * ((1/s_r) * s_c) (cpp:324-325) or ((1/s_r) * x) * s_c (main.py),
+        # with the reciprocals the ring holds
+        if order == 0:
+            return a * (inv_rows[:, None] * s_cols[None, :])
+        return (inv_rows[:, None] * a) * s_cols[None, :]
+
+    def round_deferred(self, mat, s_cur, inv_cur, s_next, inv_next, v, pend_s, pend_inv,
+                       row0, eps, k, max_itr, semantics, st, store, flush=False):
+        e = st.get("end", 0)
+        if e and e <= k and not flush:
+            return
+        nr = mat.shape[0]
+        assert len(pend_s) == len(pend_inv) < self.defer_rounds(nr, mat.shape[1], mat.dtype)
+        order = 0 if semantics == _lib.ST_SEM_SYCL else 1
+        a = mat.numpy().copy()
+        for ps, pi in zip(pend_s, pend_inv):        # A_j -> A_k, oldest first
+            a = self._update(a, pi.numpy()[row0:row0 + nr], ps.numpy(), order)
+        sn = s_cur.numpy()
+        if not flush:
+            m = self.o.find_max(sn)
+            vl = v[row0:row0 + nr]
+            vl.copy_(torch.from_numpy(self.o.compute_eigen_vector(sn[row0:row0 + nr], m,
+                                                                  vl.numpy())))
+            ok = self.o.stop(sn, eps=sn.dtype.type(eps), cyclic=semantics == _lib.ST_SEM_SYCL)
+            st.update(eigen_val=float(sn[0]), max=float(m), stop=int(ok), round=k)
+            if ok:
+                st.update(done=1, end=k + 1, iters=k if semantics == _lib.ST_SEM_SYCL else k + 1)
+            elif k + 1 >= max_itr:
+                st.update(done=1, end=k + 1, iters=max_itr)
+        a = self._update(a, inv_cur.numpy()[row0:row0 + nr], sn, order)
+        if not flush:
+            rs = self.o.rowsum(np.ascontiguousarray(a))
+            s_next.copy_(torch.from_numpy(rs))
+            inv_next.copy_(torch.from_numpy(1 / rs))
+        if store:
+            mat.copy_(torch.from_numpy(a))
+            self.stores += 1
+
+
+def _defer_policy(name):
+    """(defer(nrows), rounds(nrows)) of a CpuDeferOps test case."""
+    return {
+        "all3": (lambda nr: True, lambda nr: 3),
+        "all2": (lambda nr: True, lambda nr: 2),
+        # n = 101 over 3 ranks: blocks of 34, 34, 33 rows; the short last
+        # block does not defer, the others do with different m
+        "uneven": (lambda nr: nr >= 34, lambda nr: 3 if nr % 2 == 0 else 4),
+        # n = 101 over 2 ranks: 51 + 50 rows, m = 4 and 2
+        "mixed_m": (lambda nr: True, lambda nr: 4 if nr % 2 else 2),
+    }[name]
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -159,17 +236,21 @@ def _free_port():
 
 
 def _worker(rank, world, port, n, kind, dtype, semantics, outdir, matrix_free=False,
-            overlap=False):
+            overlap=False, defer=None, max_itr=1000, eps=1e-3):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        sh = ShardedSimilarityTransform(n, dtype, ops=CpuShardOps(), semantics=semantics,
+        ops = CpuShardOps() if defer is None else CpuDeferOps(*_defer_policy(defer))
+        sh = ShardedSimilarityTransform(n, dtype, ops=ops, semantics=semantics,
                                         matrix_free=matrix_free, overlap=overlap)
         sh.load(kind, seed=3)
-        lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=3)
+        lam, v, iters, rounds = sh.solve(eps=eps, max_itr=max_itr, batch=3)
         np.save(os.path.join(outdir, f"v{rank}.npy"), v.numpy())
         np.save(os.path.join(outdir, f"meta{rank}.npy"),
-                np.array([lam, iters, rounds, sh.part.row0, sh.part.nrows], dtype=np.float64))
+                np.array([lam, iters, rounds, sh.part.row0, sh.part.nrows,
+                          int(sh.deferred_writes), getattr(ops, "stores", -1)],
+                         dtype=np.float64))
+        np.save(os.path.join(outdir, f"a{rank}.npy"), sh.mat.numpy())
     finally:
         dist.destroy_process_group()
 
@@ -200,7 +281,7 @@ def test_sharded_solve_bit_identical_to_oracle(tmp_path, orc, world, n, kind, dt
     mat = orc.hilbert(n, npdt) if kind == "hilbert" else orc.random_matrix(n, 3, npdt)
     ref = orc.similarity_transform(mat, semantics)
     for r in range(world):
-        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")
+        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")[:5]
         v = np.load(tmp_path / f"v{r}.npy")
         assert int(iters) == ref.iter_count
         assert int(rounds) == ref.rounds_evaluated
@@ -217,7 +298,7 @@ def test_sharded_matrix_free_matches_oracle(tmp_path, orc, world, n):
     ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL)
     v0 = np.load(tmp_path / "v0.npy")
     for r in range(world):
-        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")
+        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")[:5]
         assert int(iters) == ref.iter_count and int(rounds) == ref.rounds_evaluated
         assert abs(lam - ref.eigen_val) <= 1e-12 * ref.eigen_val
         v = np.load(tmp_path / f"v{r}.npy")
@@ -241,7 +322,7 @@ def test_sharded_overlap_matches_oracle(tmp_path, orc, world, n, kind, semantics
     ref = orc.similarity_transform(mat, semantics)
     v0 = np.load(tmp_path / "v0.npy")
     for r in range(world):
-        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")
+        lam, iters, rounds, row0, nrows = np.load(tmp_path / f"meta{r}.npy")[:5]
         v = np.load(tmp_path / f"v{r}.npy")
         assert int(iters) == ref.iter_count and int(rounds) == ref.rounds_evaluated
         assert np.array_equal(v, v0)                      # identical on every rank
@@ -256,3 +337,61 @@ def test_overlap_rejects_matrix_free():
     with pytest.raises(ValueError):
         ShardedSimilarityTransform(64, torch.float64, ops=CpuShardOps(), matrix_free=True,
                                    overlap=True)
+
+
+def _oracle_final_matrix(orc, mat, semantics, end):
+    """A_end of the every-round loop: `end` transforms, each from the row sums
+    of the matrix before it (what the device solve leaves in place)."""
+    a = mat.copy()
+    order = 0 if semantics == _lib.ST_SEM_SYCL else 1
+    for _ in range(end):
+        a = orc.compute_next(a, orc.rowsum(a), order=order)
+    return a
+
+
+@pytest.mark.parametrize("world,n,kind,dtype,semantics,policy,max_itr,eps", [
+    (2, 128, "hilbert", torch.float64, _lib.ST_SEM_SYCL, "all3", 1000, 1e-3),
+    (3, 101, "random", torch.float64, _lib.ST_SEM_SYCL, "uneven", 1000, 1e-3),
+    (3, 101, "hilbert", torch.float64, _lib.ST_SEM_MAINPY, "uneven", 1000, 1e-3),
+    (2, 101, "random", torch.float64, _lib.ST_SEM_SYCL, "mixed_m", 1000, 1e-3),
+    (2, 256, "hilbert", torch.float32, _lib.ST_SEM_SYCL, "all2", 1000, 1e-3),
+    # fixed round counts ending at every residue of the rounds per store
+    (3, 101, "random", torch.float64, _lib.ST_SEM_SYCL, "uneven", 7, 0.0),
+    (3, 101, "random", torch.float64, _lib.ST_SEM_SYCL, "uneven", 8, 0.0),
+    (2, 101, "hilbert", torch.float64, _lib.ST_SEM_SYCL, "mixed_m", 9, 0.0),
+    (2, 101, "hilbert", torch.float64, _lib.ST_SEM_SYCL, "mixed_m", 10, 0.0),
+])
+def test_sharded_deferred_writes_bit_identical_to_oracle(tmp_path, orc, world, n, kind, dtype,
+                                                         semantics, policy, max_itr, eps):
+    """The driver's deferred-write solve (ShardedSimilarityTransform._solve_deferred,
+    the default for GPU blocks of >= 144 MiB) at world sizes 2 and 3 with
+    uneven last blocks, ranks that do and do not defer in the same solve and
+    ranks with different rounds per store: λ, v, the iteration count AND every
+    rank's final row block are bit-identical to the oracle's every-round
+    loop (the ring of gathered s / own-row 1/s and the final flush are
+    exercised)."""
+    mp.spawn(_worker, args=(world, _free_port(), n, kind, dtype, semantics, str(tmp_path),
+                            False, False, policy, max_itr, eps), nprocs=world, join=True)
+    npdt = np.float64 if dtype == torch.float64 else np.float32
+    mat = orc.hilbert(n, npdt) if kind == "hilbert" else orc.random_matrix(n, 3, npdt)
+    ref = orc.similarity_transform(mat, semantics, eps=npdt(eps), max_itr=max_itr)
+    a_end = _oracle_final_matrix(orc, mat, semantics, ref.rounds_evaluated)
+    defer_of, rounds_of = _defer_policy(policy)
+    saw_defer = saw_plain = False
+    for r in range(world):
+        lam, iters, rounds, row0, nrows, deferred, stores = np.load(tmp_path / f"meta{r}.npy")
+        row0, nrows = int(row0), int(nrows)
+        assert bool(deferred) == defer_of(nrows)
+        saw_defer |= bool(deferred)
+        saw_plain |= not bool(deferred)
+        if deferred:   # one store per m rounds plus the flush of a partial group
+            m = rounds_of(nrows)
+            assert int(stores) == -(-int(rounds) // m)
+        v = np.load(tmp_path / f"v{r}.npy")
+        assert int(iters) == ref.iter_count
+        assert int(rounds) == ref.rounds_evaluated
+        assert npdt(lam) == ref.eigen_val
+        assert np.array_equal(v, ref.eigen_vec)
+        assert np.array_equal(np.load(tmp_path / f"a{r}.npy"), a_end[row0:row0 + nrows])
+    if policy == "uneven":
+        assert saw_defer and saw_plain
