@@ -3,37 +3,50 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n N0]
                     [--kind hilbert|random] [--dtype f64|f32] [--no-cpu]
-                    [--no-north-star]
+                    [--no-north-star] [--no-headline] [--strong] [--one-gpu]
 
 One *step* = one round of the hot path on the HBM-resident matrix: the
 single fused launch (max / eigenvector update / stop test of s_k, then
 A_{k+1} = D^-1 A_k D in place and its row sums) that moves 2*N^2*b bytes
 (read A_k, write A_{k+1}), plus, for N > 1 GPUs, the all-gather of the
-row-sum vector.  The stop
-tolerance is set to 0 inside the timed region so that every one of the K
-rounds does the full work (after convergence the reference would stop;
-a fixed round count is how SURVEY.md §8d prices ms/iteration).
+row-sum vector.  The stop tolerance is set to 0 inside the timed region so
+that every one of the K rounds does the full work (after convergence the
+reference would stop; a fixed round count is how SURVEY.md §8d prices
+ms/iteration).
+
+Launch: `--gpus N` with N > 1 runs one process per GPU.  Under
+torch.distributed.run (WORLD_SIZE set) this process is one rank; without it
+this process starts the N ranks itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / a free MASTER_PORT in their environment) and exits
+with their status, never touching a GPU itself.
 
 Workload (config.workload): BASELINE.json configs[1], 8192x8192 Hilbert
-fp64 on one GPU.  For N GPUs the row-block sharded path runs with
-per-GPU bytes held constant (weak scaling): n = 8192*sqrt(N) rounded to a
-multiple of 64*N, rows split in contiguous blocks, one RCCL all-gather per
-round.  `--strong` keeps n fixed instead (configs[3]:
-`--n 65536 --kind random --strong` on 8 GPUs).  `value` = algorithmic bytes of all ranks / max-over-ranks time
-(GB/s); `ms_per_step` = ms/iteration.
+fp64 on one GPU.  For N GPUs the row-block sharded path runs with per-GPU
+bytes held constant (weak scaling): n = 8192*sqrt(N) rounded to a multiple
+of 64*N, rows split in contiguous blocks, one RCCL all-gather per round.
+`--strong` keeps n fixed instead.  `value` = algorithmic bytes of all ranks
+/ max-over-ranks time (GB/s); `ms_per_step` = ms/iteration.
 
-Extra objects on the JSON line: `roofline` (fused kernel, HIP events on
-the launch stream), `cpu_baseline` (the CPU oracle's 3-pass schedule on
-the host cores, rank 0 at N=1), `solve` (the reference-semantics solve to
-convergence: rounds, λ), `matrix_free` (the read-only form of the same
-iteration, SURVEY.md §8f item 1, priced against its own N^2*b bytes),
-`north_star` (32768x32768 random fp64, 1 GPU, both forms),
-`deferred_writes` (the library's solve loop, which stores the matrix every
-m-th round — 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32 (st_defer_rounds) —
-with bit-identical results, against storing every
-round; priced against its own (m+1)/m*N^2*b bytes) and, under
-`reference_headline`, `config0_hilbert128_gpu` (configs[0]'s 128^2 Hilbert
-solved on the GPU in one workgroup launch).
+Extra objects on the JSON line:
+  roofline         the round's kernels (HIP events on the launch stream)
+  solve            the reference-semantics solve to convergence (rounds, λ)
+  matrix_free      the read-only form of the iteration,
+                   priced against its own N^2*b bytes
+  configs3_strong  (N > 1) BASELINE configs[3]: 65536^2 random fp64,
+                   rows_per_gpu = 65536/N, one all-gather per round, checked
+                   against the oracle's solve and the P = 1 count
+  configs3_p1      (N = 1) the same matrix on one GPU: the strong-scaling
+                   anchor (also `configs3_p1_ms_per_iteration`)
+  north_star       (N = 1) 32768^2 random fp64, both forms
+  configs4_f32     (N = 1) 32768^2 random fp32: every-round roofline, the
+                   deferred-write rounds, the fp32-vs-fp64 tolerance study
+  deferred_writes  (N = 1) the solve loop's form (A stored every m-th
+                   round, bit-identical), timed with HIP events over whole
+                   store cycles, priced against (m+1)/m*N^2*b
+  reference_headline  the reference's own published whole-solve table
+  cpu_baseline     the oracle's 3-pass schedule on every host core
+`--one-gpu` (all ranks on cuda:0, a plumbing rehearsal) marks the line
+"representative": false and drops every roofline fraction.
 """
 from __future__ import annotations
 
@@ -41,6 +54,8 @@ import argparse
 import json
 import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -52,9 +67,10 @@ MALL_BYTES = 256 << 20  # memory-side (Infinity) cache
 # fp64 Hilbert 8192, reference semantics (cyclic, EPS=1e-3): 17 rounds,
 # λ = 2.5999921826283514 (CPU oracle; README.md:76 publishes 17 rounds)
 HILBERT8192_F64 = (17, 2.5999921826283514)
+BIG = 2 ** 31           # max_itr of the timed rounds (never reached)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
@@ -63,14 +79,17 @@ def parse():
     p.add_argument("--kind", default="hilbert", choices=["hilbert", "random"])
     p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     p.add_argument("--no-cpu", action="store_true")
-    p.add_argument("--no-north-star", action="store_true")
+    p.add_argument("--no-north-star", action="store_true",
+                   help="skip the full-size legs (north_star, configs3, configs4_f32, "
+                        "deferred_writes, the CPU's 32768^2 sample)")
+    p.add_argument("--no-configs3", action="store_true",
+                   help="skip the 65536^2 configs[3] leg")
     p.add_argument("--no-headline", action="store_true",
                    help="skip the fp32 whole-solve comparison with the published numbers")
     p.add_argument("--cpu-seconds", type=float, default=15.0,
                    help="CPU baseline sample length (rounds are calibrated to it)")
     p.add_argument("--strong", action="store_true",
-                   help="keep n fixed for every N (strong scaling; e.g. configs[3]: "
-                        "--n 65536 --kind random --strong)")
+                   help="keep n fixed for every N (strong scaling)")
     p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                    help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     p.add_argument("--overlap", action="store_true",
@@ -79,8 +98,52 @@ def parse():
     p.add_argument("--no-overlap-leg", action="store_true",
                    help="N > 1: skip the extra overlapped-exchange leg")
     p.add_argument("--one-gpu", action="store_true",
-                   help="rehearsal: every rank on cuda:0 (use with --backend gloo)")
-    return p.parse_args()
+                   help="rehearsal: every rank on cuda:0 (use with --backend gloo); the "
+                        "line is marked non-representative")
+    return p.parse_args(argv)
+
+
+# ---------------------------------------------------------------------------
+# launch
+# ---------------------------------------------------------------------------
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """Start the N ranks of `bench.py argv` as child processes (this parent
+    never initialises a GPU) and return the worst exit status.  A rank that
+    fails ends the others (by their own PIDs)."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                      env=env))
+    rcs = [None] * n
+    while any(rc is None for rc in rcs):
+        for i, pr in enumerate(procs):
+            if rcs[i] is None:
+                rcs[i] = pr.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            for i, pr in enumerate(procs):
+                if rcs[i] is None:
+                    pr.terminate()
+            for i, pr in enumerate(procs):
+                if rcs[i] is None:
+                    try:
+                        rcs[i] = pr.wait(timeout=30)
+                    except subprocess.TimeoutExpired:
+                        pr.kill()
+                        rcs[i] = pr.wait()
+            break
+        time.sleep(0.2)
+    bad = [rc for rc in rcs if rc != 0]
+    return (bad[0] if bad[0] > 0 else 1) if bad else 0
 
 
 def scaled_n(n1: int, world: int) -> int:
@@ -90,10 +153,12 @@ def scaled_n(n1: int, world: int) -> int:
     return int(round(n1 * math.sqrt(world) / q)) * q
 
 
+# ---------------------------------------------------------------------------
+# committed evidence read by the line
+# ---------------------------------------------------------------------------
 def true_lambda(n, dtype, seed):
     """Committed CPU Perron root (tests/golden/large_pins.json) or None."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "golden",
-                        "large_pins.json")
+    path = os.path.join(HERE, "tests", "golden", "large_pins.json")
     try:
         for c in json.load(open(path))["cases"]:
             if (c["n"], c["dtype"], c["seed"]) == (n, dtype, seed):
@@ -101,6 +166,16 @@ def true_lambda(n, dtype, seed):
     except (OSError, ValueError, KeyError):
         pass
     return None
+
+
+def oracle_pin(name):
+    """The oracle's solve of a full-size seeded input
+    (tests/golden/large_oracle.json, make_large_oracle.py) or None."""
+    try:
+        return json.load(open(os.path.join(HERE, "tests", "golden",
+                                           "large_oracle.json")))["cases"][name]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def load_traffic(workload: str, kernel: str = "k_round"):
@@ -131,6 +206,31 @@ def cw_bound(torch, a0, v, lam):
     return max(abs(lam - lo), abs(lam - hi)) / abs(lam)
 
 
+def host_info() -> dict:
+    model = None
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "affinity_cpus": len(os.sched_getaffinity(0))}
+
+
+# ---------------------------------------------------------------------------
+# timing
+# ---------------------------------------------------------------------------
+def _max_over_ranks(torch, dist, world, *vals):
+    if world == 1:
+        return vals
+    t = torch.tensor(vals, dtype=torch.float64,
+                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return tuple(float(x) for x in t)
+
+
 def timed_rounds(sh, steps, warmup, torch, dist, world):
     """Warmup + K timed rounds; returns (elapsed_s_max, kernel_ms_avg).
 
@@ -143,7 +243,7 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     brackets each launch with its own pair for the kernel average."""
     sh.start()
     for _ in range(warmup):
-        sh.round(0.0, 2**31)
+        sh.round(0.0, BIG)
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     if world > 1:
@@ -152,8 +252,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     t0 = time.perf_counter()
     if world == 1:
         ev[0][0].record()
-    for k in range(steps):
-        sh.round(0.0, 2**31)
+    for _ in range(steps):
+        sh.round(0.0, BIG)
     if world == 1:
         ev[0][1].record()
     torch.cuda.synchronize()
@@ -162,24 +262,320 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
     if world == 1:
-        fused = ev[0][0].elapsed_time(ev[0][1]) / steps
-    else:  # kernel-only average, outside the timed region
-        n_ev = min(steps, 50)
-        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(n_ev)]
-        for k in range(n_ev):
-            sh.round(0.0, 2**31, events=ev[k])
-        torch.cuda.synchronize()
-        fused = sum(a.elapsed_time(b) for a, b in ev) / n_ev
-        t = torch.tensor([el, fused], dtype=torch.float64,
-                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el, fused = float(t[0]), float(t[1])
-    return el, fused
+        return el, ev[0][0].elapsed_time(ev[0][1]) / steps
+    n_ev = min(steps, 50)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(n_ev)]
+    for k in range(n_ev):
+        sh.round(0.0, BIG, events=ev[k])
+    torch.cuda.synchronize()
+    fused = sum(a.elapsed_time(b) for a, b in ev) / n_ev
+    return _max_over_ranks(torch, dist, world, el, fused)
 
 
+def timed_deferred(sh, cycles, warm_cycles, torch, dist, world):
+    """The deferred-write loop over whole store cycles: rounds k0 .. k0 +
+    cycles*m - 1 with k0 a multiple of m, i.e. starting on the first round
+    after a store (no pending scaling) and ending on a storing round, no
+    flush inside.  Returns (elapsed_s_max, event_ms_per_round, m) — HIP
+    events bracket the cycles on the launch stream."""
+    sh.deferred_start()
+    m = sh._defer_m
+    for _ in range(warm_cycles * m):
+        sh.deferred_round(0.0, BIG)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(cycles * m):
+        sh.deferred_round(0.0, BIG)
+    e1.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    ev_ms = e0.elapsed_time(e1) / (cycles * m)
+    el, ev_ms = _max_over_ranks(torch, dist, world, el, ev_ms)
+    return el, ev_ms, m
+
+
+def deferred_bitwise(sh, kind, seed, torch):
+    """2m rounds from A_0 with deferred writes and with a store every round:
+    λ, v and the final matrix bit for bit (P = 1)."""
+    m = sh._defer_m
+    sh.load(kind, seed=seed)
+    sh.deferred_start()
+    for _ in range(2 * m):
+        sh.deferred_round(0.0, BIG)
+    st_d = sh.ops.read_state(sh.state)
+    a_d, v_d = sh.mat.clone(), sh.v.clone()
+    sh.load(kind, seed=seed)
+    sh.start()
+    for _ in range(2 * m):
+        sh.round(0.0, BIG)
+    st_e = sh.ops.read_state(sh.state)
+    same = (st_d["eigen_val"] == st_e["eigen_val"] and torch.equal(v_d, sh.v)
+            and torch.equal(a_d, sh.mat))
+    del a_d, v_d
+    return bool(same)
+
+
+def profile_cycle_ms(workload: str):
+    """Sum over one store cycle of the committed rocprof averages of the
+    deferred flat round (k_flat per pending count NP + k_parts per round),
+    from profiles/*_defer_cycle_*.json (tools/defer_profile.py --json)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_defer_cycle_*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("workload") == workload:
+            best = (d["cycle_ms_per_round"], os.path.relpath(f, HERE))
+    return best
+
+
+# ---------------------------------------------------------------------------
+# legs
+# ---------------------------------------------------------------------------
+def rate(bytes_, ms):
+    return bytes_ / (ms * 1e-3) / 1e9
+
+
+def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representative):
+    """BASELINE configs[3]: 65536^2 random fp64 row-block sharded over the
+    world (P = 1: the whole 32 GiB on one GPU), one all-gather per round:
+    the reference-semantics solve checked against the oracle's solve of the
+    same matrix (tests/golden/large_oracle.json: iteration count = the P = 1
+    count, λ) and the true Perron root, then K timed every-round steps and
+    whole store cycles of the solve loop's deferred-write form."""
+    n = 65536
+    sh = sharded.ShardedSimilarityTransform(n, torch.float64)
+    p = sh.part
+    sh.load("random", seed=0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lam, v, it, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=1)
+    torch.cuda.synchronize()
+    solve_ms = (time.perf_counter() - t0) * 1e3
+    pin, perron = oracle_pin("random65536_f64"), true_lambda(n, "f64", 0)
+    check = {}
+    if pin is not None:
+        check.update(oracle_iter_count=pin["iter_count"],
+                     iter_count_equal=it == pin["iter_count"],
+                     eigen_val_rel_err_vs_oracle=abs(lam - pin["eigen_val"]) / pin["eigen_val"])
+    if perron is not None:
+        check["eigen_val_rel_err_vs_true"] = abs(lam - perron) / perron
+    sh.load("random", seed=0)
+    el, fused = timed_rounds(sh, steps, warmup, torch, dist, world)
+    by_total, by_local = 2.0 * n * n * 8, 2.0 * p.nrows * n * 8
+    leg = {"workload": "random65536_f64", "n": n, "rows_per_gpu": p.chunk, "n_gpus": world,
+           "ms_per_iteration": round(el / steps * 1e3, 4), "steps": steps,
+           "value": round(by_total * steps / el / 1e9, 2), "unit": "GB/s",
+           "bytes_per_round": by_total,
+           "kernel_ms_avg": round(fused, 4), "achieved": round(rate(by_local, fused), 1),
+           "solve": {"iter_count": it, "rounds_evaluated": rounds, "eigen_val": lam,
+                     "ms": round(solve_ms, 2), "check": check}}
+    if representative:
+        leg["frac"] = round(rate(by_local, fused) / HBM_PEAK_GBS, 4)
+    if sh.deferred_writes:
+        el_d, ev_d, m = timed_deferred(sh, 4, 1, torch, dist, world)
+        by_d = (m + 1.0) / m * n * n * 8
+        leg["deferred_writes"] = {"stores_every": m,
+                                  "ms_per_iteration": round(el_d / (4 * m) * 1e3, 4),
+                                  "event_ms_per_round": round(ev_d, 4),
+                                  "value": round(rate(by_d, el_d / (4 * m) * 1e3), 2),
+                                  "bytes_per_round": by_d}
+    if sh.rccl is not None:
+        leg["rccl_ranks"] = sh.rccl.info()["nranks"]
+    sh.close()
+    del sh, v
+    torch.cuda.empty_cache()
+    return leg
+
+
+def deferred_leg(sharded, dev, torch, kind, n, dt, seed, every_ms):
+    """The solve loop's deferred writes at P = 1 (ShardedSimilarityTransform
+    runs the same st_round_flat_deferred launches as DeviceSolver): HIP
+    events over whole store cycles, the bitwise check against storing every
+    round, and the committed rocprof cycle sum beside it."""
+    sh = sharded.ShardedSimilarityTransform(n, dt)
+    if not sh.deferred_writes:
+        return None
+    sh.load(kind, seed=seed)
+    cycles = max(3, int(round(60.0 / max(every_ms, 1e-3) / 4)))  # ~40-60 ms of rounds
+    el, ev_ms, m = timed_deferred(sh, cycles, 2, torch, None, 1)
+    same = deferred_bitwise(sh, kind, seed, torch)
+    bpe = 8 if dt == torch.float64 else 4
+    by = (m + 1.0) / m * n * n * bpe
+    workload = f"{kind}{n}_{'f64' if bpe == 8 else 'f32'}"
+    out = {"stores_every": m, "cycles": cycles, "ms_per_iteration": round(ev_ms, 4),
+           "ms_per_iteration_host_clock": round(el / (cycles * m) * 1e3, 4),
+           "ms_per_iteration_write_every_round": round(every_ms, 4),
+           "speedup": round(every_ms / ev_ms, 3), "bytes_per_round": by,
+           "achieved": round(rate(by, ev_ms), 1),
+           "frac": round(rate(by, ev_ms) / HBM_PEAK_GBS, 4),
+           "bitwise_equal_to_write_every_round": same,
+           "timing": "HIP events around whole store cycles (first round after a store "
+                     "... the storing round), no flush inside"}
+    prof = profile_cycle_ms(workload)
+    if prof is not None:
+        out["rocprof_cycle_ms_per_round"] = prof[0]
+        out["rocprof_source"] = prof[1]
+        out["events_vs_rocprof"] = round(ev_ms / prof[0], 4)
+    sh.close()
+    del sh
+    torch.cuda.empty_cache()
+    return out
+
+
+def configs4_leg(sharded, dev, torch, np_, dist):
+    """BASELINE configs[4]: 32768^2 random fp32 on one GPU — the every-round
+    step (roofline on 2*N^2*4 bytes), the solve loop's deferred rounds, and
+    the fp32-vs-fp64 tolerance study on the same input: λ and v after 8
+    rounds against the fp64 iteration and the oracle's fp32 solve, and the
+    stop test at the reference's EPS = 1e-3f (never passes at this size)."""
+    n = 32768
+    sh = sharded.ShardedSimilarityTransform(n, torch.float32)
+    sh.load("random", seed=0)
+    el, fused = timed_rounds(sh, 50, 3, torch, dist, 1)
+    by = 2.0 * n * n * 4
+    flat = dev.flat_round_pays(n, n, torch.float32)
+    tr = load_traffic("random32768_f32", "k_flat" if flat else "k_round")
+    out = {"workload": "random32768_f32",
+           "kernel": "flat round: k_flat + k_parts (round time)" if flat else "k_round",
+           "ms_per_iteration": round(el / 50 * 1e3, 4),
+           "roofline": {"bound": "hbm", "achieved": round(rate(by, fused), 1),
+                        "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(rate(by, fused) / HBM_PEAK_GBS, 4),
+                        "traffic": None if tr is None else tr[0],
+                        "traffic_source": None if tr is None else tr[1],
+                        "fused_ms_avg": round(fused, 5), "bytes_per_launch": by}}
+    # tolerance study: 8 rounds (eps = 0) in fp32 and fp64 on the same input
+    sh.load("random", seed=0)
+    lam32, v32, it32, _ = sh.solve(eps=0.0, max_itr=8, batch=8)
+    v32 = v32.double()
+    sh.close()
+    del sh
+    torch.cuda.empty_cache()
+    sh64 = sharded.ShardedSimilarityTransform(n, torch.float64)
+    sh64.load("random", seed=0)
+    lam64, v64, it64, _ = sh64.solve(eps=0.0, max_itr=8, batch=8)
+    sh64.close()
+    del sh64
+    torch.cuda.empty_cache()
+    tol = {"rounds": 8, "eigen_val_f32": lam32, "eigen_val_f64": lam64,
+           "eigen_val_rel_diff": abs(lam32 - lam64) / lam64,
+           "eigen_vec_max_abs_diff": (v32 - v64).abs().max().item()}
+    pin = oracle_pin("random32768_f32_8rounds")
+    if pin is not None:   # the oracle's fp32 solve, EPS = 1e-3f, max_itr = 8
+        tol["eigen_val_rel_err_vs_oracle_f32"] = abs(lam32 - pin["eigen_val"]) / pin["eigen_val"]
+    perron = true_lambda(n, "f32", 0)
+    if perron is not None:
+        tol["eigen_val_rel_err_vs_true"] = abs(lam32 - perron) / perron
+    # the reference's fp32 stop test at this size: run the library's solve
+    # loop at EPS = 1e-3f to MAX_ITR
+    solver = dev.DeviceSolver(torch.device("cuda", torch.cuda.current_device()))
+    a = dev.generate("random", n, torch.float32, seed=0,
+                     device=torch.device("cuda", torch.cuda.current_device()))
+    lam_r, _, it_r, st_r = solver.solve(a, inplace=True, batch=64)
+    solver.close()
+    del a
+    torch.cuda.empty_cache()
+    tol["reference_eps"] = {"eps": 1e-3, "iter_count": it_r, "converged": bool(st_r["converged"]),
+                            "loop_ms": round(st_r["loop_ms"], 1), "eigen_val": float(lam_r)}
+    tol["study"] = "profiles/r01_fp32_study.json (per-round λ / max adjacent |Δs| tables)"
+    out["tolerance_study"] = tol
+    out["_every_ms"] = el / 50 * 1e3
+    return out
+
+
+def cpu_leg(args, np_, workload, n, bytes_round_total, ms_per_step):
+    """The oracle's 3-pass schedule (oracle/st_oracle.c: row sums, stats,
+    transform per round; OpenMP over rows) on every CPU of this process's
+    affinity mask: a bounded sample of the bench workload, configs[0]'s
+    128^2 Hilbert on one core, and (full runs) the random 32768^2 fp64
+    sample BASELINE.md §3 plans."""
+    from oracle import oracle as orc
+    info = host_info()
+    threads = info["affinity_cpus"]
+    b = 8 if args.dtype == "f64" else 4
+    npdt = np_.float64 if args.dtype == "f64" else np_.float32
+    mat = orc.generate_c(args.kind, n, 0, npdt)
+    cal = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=3, nthreads=threads)
+    est = max(cal.loop_ms / 3, 1e-3)
+    rounds_cpu = int(min(5000, max(3, args.cpu_seconds * 1e3 / est)))
+    r = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=rounds_cpu, nthreads=threads)
+    # every round = row-sum pass + stats + transform pass: the CPU moves
+    # 3*N^2*b per round (read, read, write); `value` uses the GPU line's
+    # 2*N^2*b accounting so the two are comparable
+    per_round_ms = r.loop_ms / rounds_cpu
+    solve_cpu = orc.similarity_transform(mat, orc.SEM_SYCL, nthreads=threads)
+    del mat
+    out = {"value": round(rate(bytes_round_total, per_round_ms), 3), "unit": "GB/s",
+           "ms_per_iteration": round(per_round_ms, 3), "cores": threads, "kind": "port",
+           "sample": f"{workload}: {rounds_cpu} rounds (eps=0, {r.loop_ms / 1e3:.1f} s) of the "
+                     "reference's 3-pass schedule (oracle/st_oracle.c, gcc -O3, OpenMP over "
+                     f"rows, {threads} threads)",
+           "traffic_rate_3pass": round(rate(1.5 * bytes_round_total, per_round_ms), 3),
+           "solve_ms": round(solve_cpu.loop_ms, 2), "solve_iter_count": solve_cpu.iter_count,
+           **info}
+    out["_per_round_ms"] = per_round_ms
+    if not args.no_north_star:
+        n2 = 32768
+        m2 = orc.generate_c("random", n2, 0, np_.float64)
+        rr = orc.similarity_transform(m2, orc.SEM_SYCL, eps=0.0, max_itr=3, nthreads=threads)
+        del m2
+        ms2 = rr.loop_ms / 3
+        out["random32768_f64"] = {"rounds": 3, "ms_per_iteration": round(ms2, 2),
+                                  "value": round(rate(2.0 * n2 * n2 * 8, ms2), 2),
+                                  "traffic_rate_3pass": round(rate(3.0 * n2 * n2 * 8, ms2), 2),
+                                  "threads": threads}
+    # configs[0]: 128x128 Hilbert on the CPU path (SURVEY.md §8d config 1):
+    # the C restatement on one core (fp64 / fp32, the SYCL loop), a numpy
+    # restatement of main.py's loop, eigenvalues against eigvalsh
+    h64 = orc.hilbert(128)
+    true128 = float(np_.max(np_.linalg.eigvalsh(h64)))
+    c64 = orc.similarity_transform(h64, orc.SEM_SYCL, nthreads=1)
+    c32 = orc.similarity_transform(orc.hilbert(128, np_.float32), orc.SEM_SYCL, nthreads=1)
+    t0 = time.perf_counter()
+    a, v, itr = h64.copy(), np_.ones(128), 0
+    for itr in range(1000):          # main.py:30-47, elementwise (no O(N^3) matmul)
+        s_ = a.sum(axis=1)
+        v = v * (s_ / s_.max())
+        if np_.all(np_.abs(np_.diff(s_)) < 1e-3):
+            break
+        a = (a / s_[:, None]) * s_[None, :]
+    np_ms = (time.perf_counter() - t0) * 1e3
+    out["config1_hilbert128"] = {
+        "c_1core_f64": {"ms": round(c64.loop_ms, 4), "iter_count": c64.iter_count,
+                        "rel_err_vs_eigvalsh": abs(c64.eigen_val - true128) / true128},
+        "c_1core_f32": {"ms": round(c32.loop_ms, 4), "iter_count": c32.iter_count},
+        "numpy_mainpy_semantics": {"ms": round(np_ms, 3), "iter_count": itr + 1,
+                                   "eigen_val": float(s_[0])}}
+    return out
+
+
+def strip_fracs(obj):
+    """Drop every roofline fraction (one-GPU rehearsals share one card)."""
+    if isinstance(obj, dict):
+        return {k: strip_fracs(v) for k, v in obj.items() if k not in ("frac", "target_frac")}
+    if isinstance(obj, list):
+        return [strip_fracs(v) for v in obj]
+    return obj
+
+
+# ---------------------------------------------------------------------------
 def main():
     args = parse()
+    world_env = os.environ.get("WORLD_SIZE")
+    if args.gpus > 1 and world_env is None:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -188,11 +584,12 @@ def main():
     from eigen_value_amd import _lib
     from eigen_value_amd import device as dev
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    world = int(world_env or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    representative = not args.one_gpu
     dev_index = 0 if args.one_gpu else local
     torch.cuda.set_device(dev_index)
     if world > 1:
@@ -202,6 +599,7 @@ def main():
         else:
             dist.init_process_group("gloo")
     _lib.load()   # fail loudly before anything else if the HIP library is missing
+    full = not args.no_north_star
 
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     b = 8 if args.dtype == "f64" else 4
@@ -243,7 +641,7 @@ def main():
     bytes_round_total = 2.0 * n * n * b
     bytes_round_local = 2.0 * p.nrows * n * b
     value = bytes_round_total * args.steps / el / 1e9
-    achieved = bytes_round_local / (fused_ms * 1e-3) / 1e9
+    achieved = rate(bytes_round_local, fused_ms)
     flat_pays = dev.flat_round_pays(p.nrows, n, dt)
     flat = (not args.overlap) and flat_pays
     traffic = load_traffic(workload, "k_flat" if flat else "k_round")
@@ -266,6 +664,12 @@ def main():
     if bytes_round_local / 2 <= 2 * MALL_BYTES:
         roofline["note"] = ("matrix partly resident in the 256 MB memory-side cache: an "
                             "effective rate, not an HBM-roofline claim (see north_star)")
+    exchange = None
+    if world > 1:
+        exchange = {"backend": dist.get_backend(),
+                    "collective": ("library RCCL communicator (st_allgather)" if sh.rccl
+                                   else "torch.distributed all_gather")}
+        exchange["rccl_ranks"] = sh.rccl.info()["nranks"] if sh.rccl is not None else None
 
     # ---- N > 1: the same rounds with the exchange overlapped --------------
     # (split launch: local columns while the all-gather runs on a second
@@ -296,8 +700,8 @@ def main():
                    "traffic": None if tr_mf is None else tr_mf[0],
                    "value": round(1.0 * n * n * b * args.steps / el_mf / 1e9, 2),
                    "kernel_ms_avg": round(k_mf, 5),
-                   "achieved": round(by_mf_local / (k_mf * 1e-3) / 1e9, 1),
-                   "frac": round(by_mf_local / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                   "achieved": round(rate(by_mf_local, k_mf), 1),
+                   "frac": round(rate(by_mf_local, k_mf) / HBM_PEAK_GBS, 4),
                    "bytes_per_round": 1.0 * n * n * b, "solve_iter_count": it_mf,
                    "eigen_val": lam_mf}
     mf.close()
@@ -318,23 +722,38 @@ def main():
            "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
     if args.overlap:
         out["config"]["exchange"] = "overlapped (split round, all-gather on a second stream)"
+    if exchange is not None:
+        out["exchange"] = exchange
+        out["rccl_ranks"] = exchange["rccl_ranks"]
     if overlap_leg is not None:
         out["exchange_overlap"] = overlap_leg
     sh.close()
     del sh
     torch.cuda.empty_cache()
 
+    # ---- configs[3]: 65536^2 fp64, strong-scaled over the world ----------
+    if not args.no_configs3 and (world > 1 or full):
+        leg = configs3_leg(sharded, torch, dist, world, rank, max(5, min(args.steps, 20)),
+                           min(args.warmup, 3), representative)
+        if world > 1:
+            out["configs3_strong"] = leg
+        else:
+            out["configs3_p1"] = leg
+            out["configs3_p1_ms_per_iteration"] = leg["ms_per_iteration"]
+
     # ---- north-star size: 32768^2 random fp64 on one GPU ---------------
-    if world == 1 and not args.no_north_star:
+    every_ms = {}
+    if world == 1 and full:
         ns = sharded.ShardedSimilarityTransform(32768, torch.float64)
         ns.load("random", seed=0)
         lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=1)
         ns.load("random", seed=0)
         el_ns, fused_ns = timed_rounds(ns, 50, 3, torch, dist, 1)
         by = 2.0 * 32768 * 32768 * 8
-        ach = by / (fused_ns * 1e-3) / 1e9
+        ach = rate(by, fused_ns)
         flat_ns = dev.flat_round_pays(32768, 32768, torch.float64)
         tr = load_traffic("random32768_f64", "k_flat" if flat_ns else "k_round")
+        every_ms["random32768_f64"] = el_ns / 50 * 1e3
         out["north_star"] = {"workload": "random32768_f64",
                              "kernel": ("flat round: k_flat + k_parts (round time)"
                                         if flat_ns else "k_round"),
@@ -346,6 +765,12 @@ def main():
         pin = true_lambda(32768, "f64", 0)
         if pin is not None:  # CPU Perron root of the same matrix (tests/golden)
             out["north_star"]["eigen_val_rel_err_vs_true"] = abs(lam_ns - pin) / pin
+        opin = oracle_pin("random32768_f64")
+        if opin is not None:  # the oracle's solve of the same matrix
+            out["north_star"]["check"] = {
+                "iter_count_equal_oracle": it_ns == opin["iter_count"],
+                "eigen_val_rel_err_vs_oracle": abs(lam_ns - opin["eigen_val"]) / opin["eigen_val"]}
+        ns.close()
         del ns
         torch.cuda.empty_cache()
         # the matrix-free form on the same 32768^2 input (N^2*b per round)
@@ -358,62 +783,34 @@ def main():
         out["north_star"]["matrix_free"] = {
             "traffic": None if tr_mf is None else tr_mf[0],
             "ms_per_iteration": round(el_mf / 50 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
-            "achieved": round(by_mf / (k_mf * 1e-3) / 1e9, 1),
-            "frac": round(by_mf / (k_mf * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "achieved": round(rate(by_mf, k_mf), 1),
+            "frac": round(rate(by_mf, k_mf) / HBM_PEAK_GBS, 4),
             "bytes_per_round": by_mf, "solve_iter_count": it_mf,
             "eigen_val_rel_diff_vs_transform": abs(lam_mf - lam_ns) / lam_ns}
+        mf.close()
         del mf
         torch.cuda.empty_cache()
 
-    # ---- deferred writes: the library's solve loop (flat round, >= 144 MiB)
-    # stores A every m-th round (st_defer_rounds) and re-applies the pending
-    # scalings in registers, bit-identical to storing every round.  Per-round time from
-    # the host clock of whole solves of 10 and 40 fixed rounds (eps = 0), the
-    # difference over 30 rounds; the same with ST_FLAG_WRITE_EVERY_ROUND.
-    if world == 1 and not args.no_north_star:
-        solver = dev.DeviceSolver(torch.device("cuda", dev_index))
+        # ---- configs[4]: 32768^2 fp32 ----------------------------------
+        c4 = configs4_leg(sharded, dev, torch, np, dist)
+        every_ms["random32768_f32"] = c4.pop("_every_ms")
+        out["configs4_f32"] = c4
+
+        # ---- deferred writes: the solve loop's form (flat blocks) -------
         deferred = {}
-        for name, kind, nn, ddt in (("configs[1] " + workload, args.kind, n, dt),
-                                    ("north_star random32768_f64", "random", 32768,
-                                     torch.float64),
-                                    ("configs[4] random32768_f32", "random", 32768,
-                                     torch.float32)):
-            a0 = dev.generate(kind, nn, ddt, seed=0, device=torch.device("cuda", dev_index))
-            if not dev.flat_round_pays(nn, nn, a0.dtype):
-                continue
-            bpe = a0.element_size()
-            per, res = {}, {}
-            for every in (False, True):
-                t = {}
-                for kk in (10, 40):
-                    best = float("inf")
-                    for _ in range(3):
-                        a = a0.clone()
-                        torch.cuda.synchronize()
-                        t0 = time.perf_counter()
-                        r = solver.solve(a, inplace=True, eps=0.0, max_itr=kk,
-                                         write_every_round=every)
-                        best = min(best, time.perf_counter() - t0)
-                        if kk == 10:
-                            res[every] = (r[0], r[1].clone(), a.clone() if nn <= 8192 else None)
-                        del a
-                    t[kk] = best
-                per[every] = (t[40] - t[10]) / 30 * 1e3
-            same = (res[False][0] == res[True][0] and torch.equal(res[False][1], res[True][1])
-                    and (res[False][2] is None or torch.equal(res[False][2], res[True][2])))
-            every_m = dev.defer_rounds(nn, nn, a0.dtype)
-            by = (every_m + 1.0) / every_m * nn * nn * bpe
-            deferred[name] = {
-                "stores_every": every_m, "ms_per_iteration": round(per[False], 4),
-                "ms_per_iteration_write_every_round": round(per[True], 4),
-                "speedup": round(per[True] / per[False], 3),
-                "bytes_per_round": by, "achieved": round(by / (per[False] * 1e-3) / 1e9, 1),
-                "frac": round(by / (per[False] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                "bitwise_equal_to_write_every_round": bool(same)}
-            del a0, res
-            torch.cuda.empty_cache()
-        solver.close()
+        for name, kind, nn, ddt, key in (
+                ("configs[1] " + workload, args.kind, n, dt, None),
+                ("north_star random32768_f64", "random", 32768, torch.float64,
+                 "random32768_f64"),
+                ("configs[4] random32768_f32", "random", 32768, torch.float32,
+                 "random32768_f32")):
+            em = every_ms.get(key, el / args.steps * 1e3) if key else el / args.steps * 1e3
+            leg = deferred_leg(sharded, dev, torch, kind, nn, ddt, 0, em)
+            if leg is not None:
+                deferred[name] = leg
         out["deferred_writes"] = deferred
+        if "configs[4] random32768_f32" in deferred:
+            out["configs4_f32"]["deferred_writes"] = deferred["configs[4] random32768_f32"]
 
     # ---- the reference's own headline, apples to apples ----------------
     # README.md:66-158 of the reference publishes whole solves of the fp32
@@ -441,9 +838,9 @@ def main():
         # (k_solve_small); the per-round launch loop beside it
         c0 = {}
         with EigenValue() as e:
-            for name, dt in (("f32", np.float32), ("f64", np.float64)):
-                h = (dt(1.0) / (np.arange(128)[:, None] + np.arange(128)[None, :] + 1)
-                     .astype(dt))
+            for name, ndt in (("f32", np.float32), ("f64", np.float64)):
+                h = (ndt(1.0) / (np.arange(128)[:, None] + np.arange(128)[None, :] + 1)
+                     .astype(ndt))
                 e.similarity_transform(h)                    # warm
                 one = min((e.similarity_transform_ex(h) for _ in range(5)),
                           key=lambda r: r[4]["loop_ms"])
@@ -456,53 +853,16 @@ def main():
 
     # ---- CPU baseline (rank 0, N = 1) ------------------------------------
     if world == 1 and rank == 0 and not args.no_cpu:
-        from oracle import oracle as orc
-        threads = min(16, len(os.sched_getaffinity(0)))
-        npdt = np.float64 if args.dtype == "f64" else np.float32
-        mat = orc.hilbert(n, npdt) if args.kind == "hilbert" else orc.random_matrix(n, 0, npdt)
-        # bounded sample: calibrate on 3 rounds, then ~--cpu-seconds of rounds
-        cal = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=3, nthreads=threads)
-        est = max(cal.loop_ms / 3, 1e-3)
-        rounds_cpu = int(min(5000, max(3, args.cpu_seconds * 1e3 / est)))
-        r = orc.similarity_transform(mat, orc.SEM_SYCL, eps=0.0, max_itr=rounds_cpu,
-                                     nthreads=threads)
-        # every round = row-sum pass + stats + transform pass (the last round's
-        # transform is skipped, as in the reference loop); priced with the same
-        # 2*N^2*b accounting as `value`
-        per_round_ms = r.loop_ms / rounds_cpu
-        solve_cpu = orc.similarity_transform(mat, orc.SEM_SYCL, nthreads=threads)
-        out["cpu_baseline"] = {"value": round(bytes_round_total / (per_round_ms * 1e-3) / 1e9, 3),
-                               "unit": "GB/s", "ms_per_iteration": round(per_round_ms, 3),
-                               "cores": threads, "kind": "port",
-                               "sample": f"{workload}: {rounds_cpu} rounds (eps=0, "
-                                         f"{r.loop_ms / 1e3:.1f} s) of the reference's 3-pass "
-                                         "schedule (oracle/st_oracle.c, gcc -O3, OpenMP over rows)",
-                               "solve_ms": round(solve_cpu.loop_ms, 2),
-                               "solve_iter_count": solve_cpu.iter_count}
-        out["speedup_vs_cpu"] = round(out["ms_per_step"] and per_round_ms / out["ms_per_step"], 1)
-        # configs[0]: 128x128 Hilbert on the CPU path:
-        # the C restatement on one core (fp64 / fp32, the SYCL loop), a numpy
-        # restatement of main.py's loop, eigenvalues against eigvalsh
-        h64 = orc.hilbert(128)
-        true128 = float(np.max(np.linalg.eigvalsh(h64)))
-        c64 = orc.similarity_transform(h64, orc.SEM_SYCL, nthreads=1)
-        c32 = orc.similarity_transform(orc.hilbert(128, np.float32), orc.SEM_SYCL, nthreads=1)
-        t0 = time.perf_counter()
-        a, v, itr = h64.copy(), np.ones(128), 0
-        for itr in range(1000):          # main.py:30-47, elementwise (no O(N^3) matmul)
-            s_ = a.sum(axis=1)
-            v = v * (s_ / s_.max())
-            if np.all(np.abs(np.diff(s_)) < 1e-3):
-                break
-            a = (a / s_[:, None]) * s_[None, :]
-        np_ms = (time.perf_counter() - t0) * 1e3
-        out["cpu_baseline"]["config1_hilbert128"] = {
-            "c_1core_f64": {"ms": round(c64.loop_ms, 4), "iter_count": c64.iter_count,
-                            "rel_err_vs_eigvalsh": abs(c64.eigen_val - true128) / true128},
-            "c_1core_f32": {"ms": round(c32.loop_ms, 4), "iter_count": c32.iter_count},
-            "numpy_mainpy_semantics": {"ms": round(np_ms, 3), "iter_count": itr + 1,
-                                       "eigen_val": float(s_[0])}}
+        cb = cpu_leg(args, np, workload, n, bytes_round_total, out["ms_per_step"])
+        per_round_ms = cb.pop("_per_round_ms")
+        out["cpu_baseline"] = cb
+        out["speedup_vs_cpu"] = round(per_round_ms / out["ms_per_step"], 1)
 
+    if not representative:
+        out = strip_fracs(out)
+        out["representative"] = False
+        out["note"] = ("--one-gpu rehearsal: every rank shares cuda:0; plumbing only, not "
+                       "scaling data")
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -391,6 +391,72 @@ class ShardedSimilarityTransform:
         self.gather(self.v)
         return self.v[:self.n]
 
+    # -- deferred writes: the solve loop's form for flat blocks ------------
+    def _defer_ring(self):
+        p = self.part
+        m = self.ops.defer_rounds(p.nrows, p.n, self.dtype)
+        if self._ring is None or len(self._ring[0]) != m + 1:
+            self._ring = ([self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(m + 1)],
+                          [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(m + 1)])
+        return m
+
+    def _pending(self, j0: int, count: int):
+        """Full row-sum vectors s_j0 .. s_{j0+count-1} and their reciprocals."""
+        rs, ri = self._ring
+        R, n = len(rs), self.part.n
+        return ([rs[(j0 + i) % R][:n] for i in range(count)],
+                [ri[(j0 + i) % R][:n] for i in range(count)])
+
+    def deferred_start(self):
+        """Initial pass of the deferred-write loop: v = 1, state = 0,
+        s_0 = rowsum(A_0) gathered into ring slot 0, and 1/s_0."""
+        p = self.part
+        self._defer_m = self._defer_ring()
+        rs, ri = self._ring
+        self.ops.reset_state(self.state)
+        self.ops.fill(self.v, 1.0)
+        self.ops.rowsum(self.mat, self._slot(rs[0]))
+        self.gather(rs[0])
+        self.ops.recip(rs[0][:p.n], ri[0][:p.n])
+        self.k = 0
+
+    def deferred_round(self, eps: float, max_itr: int, events=None):
+        """Round k of the deferred-write loop (st_round_flat_deferred): the
+        block holds the last stored A_j, j = the last multiple of m <= k;
+        round k re-applies rounds j .. k-1 in registers, stores A_{k+1} when
+        k + 1 is a multiple of m, then the all-gather of s_{k+1}.  After
+        rounds 0 .. c*m - 1 the block holds A_{c*m}, exactly as c*m calls of
+        round() leave it."""
+        p, m, k = self.part, self._defer_m, self.k
+        rs, ri = self._ring
+        R = len(rs)
+        cur, nxt, j0 = k % R, (k + 1) % R, k - k % m
+        ps, pi = self._pending(j0, k - j0)
+        if events is not None:
+            events[0].record()
+        self.ops.round_deferred(self.mat, rs[cur][:p.n], ri[cur][:p.n], self._slot(rs[nxt]),
+                                ri[nxt][p.row0:p.row0 + p.nrows], self.v, ps, pi,
+                                p.row0, eps, k, max_itr, self.semantics, self.state,
+                                store=(k - j0 + 1 == m))
+        if events is not None:
+            events[1].record()
+        self.gather(rs[nxt])
+        self.k = k + 1
+
+    def deferred_flush(self, end: int, eps: float, max_itr: int):
+        """After the loop stopped at round end - 1: store A_end if the last
+        group was partial (the block then holds what round() would leave)."""
+        p, m = self.part, self._defer_m
+        if end % m == 0:
+            return
+        rs, ri = self._ring
+        R, kl = len(rs), end - 1
+        j0 = kl - kl % m
+        ps, pi = self._pending(j0, kl - j0)
+        self.ops.round_deferred(self.mat, rs[kl % R][:p.n], ri[kl % R][:p.n], None, None,
+                                self.v, ps, pi, p.row0, eps, kl, max_itr, self.semantics,
+                                self.state, store=True, flush=True)
+
     def _solve_deferred(self, eps: float, max_itr: int, batch: int):
         """solve() with deferred writes (st_round_flat_deferred): the block is
         stored every m-th round and the rounds in between re-apply the pending
@@ -398,46 +464,17 @@ class ShardedSimilarityTransform:
         pending rounds kept in a ring of m + 1 vectors (and their reciprocals).
         One all-gather per round as before; bit-identical results; a final
         flush leaves the block as storing every round would."""
-        p = self.part
-        m = self.ops.defer_rounds(p.nrows, p.n, self.dtype)
-        R = m + 1
-        if self._ring is None:
-            self._ring = ([self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(R)],
-                          [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(R)])
-        rs, ri = self._ring
-        full = lambda x: x[:p.n]                         # noqa: E731
-        pend = lambda j0, n_: ([full(rs[(j0 + i) % R]) for i in range(n_)],  # noqa: E731
-                               [full(ri[(j0 + i) % R]) for i in range(n_)])
-        self.ops.reset_state(self.state)
-        self.ops.fill(self.v, 1.0)
-        self.ops.rowsum(self.mat, self._slot(rs[0]))
-        self.gather(rs[0])
-        self.ops.recip(full(rs[0]), full(ri[0]))
-        k = 0
-        while k < max_itr:
-            for _ in range(min(batch, max_itr - k)):
-                cur, nxt, j0 = k % R, (k + 1) % R, k - k % m
-                ps, pi = pend(j0, k - j0)
-                self.ops.round_deferred(self.mat, full(rs[cur]), full(ri[cur]),
-                                        self._slot(rs[nxt]),
-                                        ri[nxt][p.row0:p.row0 + p.nrows], self.v, ps, pi,
-                                        p.row0, eps, k, max_itr, self.semantics, self.state,
-                                        store=(k - j0 + 1 == m))
-                self.gather(rs[nxt])
-                k += 1
+        self.deferred_start()
+        while self.k < max_itr:
+            for _ in range(min(batch, max_itr - self.k)):
+                self.deferred_round(eps, max_itr)
             if self.ops.read_state(self.state)["done"]:
                 break
         st = self.ops.read_state(self.state)
         if not st["done"]:
             raise _lib.EigenValueError("sharded solve ended without done flag")
         end = st["end"]
-        if end % m:
-            kl = end - 1
-            j0 = kl - kl % m
-            ps, pi = pend(j0, kl - j0)
-            self.ops.round_deferred(self.mat, full(rs[kl % R]), full(ri[kl % R]), None, None,
-                                    self.v, ps, pi, p.row0, eps, kl, max_itr, self.semantics,
-                                    self.state, store=True, flush=True)
+        self.deferred_flush(end, eps, max_itr)
         self.k = end
         return st["eigen_val"], self.eigen_vector(end), st["iters"], end
 

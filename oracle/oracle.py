@@ -75,6 +75,9 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"orc_similarity_transform_{sfx}").argtypes = [
             P, u32, T, u32, i32, i32, P, P, P, P, P, P]
         getattr(L, f"orc_similarity_transform_{sfx}").restype = i32
+        getattr(L, f"orc_similarity_transform_gen_{sfx}").argtypes = [
+            i32, u64, u32, T, u32, i32, i32, u32, P, P, P, P, P]
+        getattr(L, f"orc_similarity_transform_gen_{sfx}").restype = i32
     L.orc_max_threads.restype = i32
 
 
@@ -206,3 +209,47 @@ def similarity_transform(mat: np.ndarray, semantics: int = SEM_SYCL, eps=None,
 
 def max_threads() -> int:
     return int(lib().orc_max_threads())
+
+
+def generate_c(kind: str, n: int, seed: int = 0, dtype=np.float64,
+               nrows: Optional[int] = None, row0: int = 0) -> np.ndarray:
+    """The C generators (orc_hilbert_* / orc_random_*, OpenMP): the same bits
+    as hilbert() / random_matrix(), without numpy's temporaries — for the
+    full-size configs (8 GiB at 32768^2 fp64)."""
+    nrows = n if nrows is None else nrows
+    out = np.empty((nrows, n), dtype=dtype)
+    L = lib()
+    if kind == "hilbert":
+        getattr(L, f"orc_hilbert_{_sfx(dtype)}")(_ptr(out), nrows, n, row0)
+    elif kind == "random":
+        getattr(L, f"orc_random_{_sfx(dtype)}")(_ptr(out), nrows, n, row0, seed)
+    else:
+        raise ValueError(f"unknown kind {kind!r}")
+    return out
+
+
+def similarity_transform_gen(kind: str, n: int, seed: int = 0, dtype=np.float64,
+                             semantics: int = SEM_SYCL, eps=None, max_itr: int = 64,
+                             nthreads: int = 0, chunk_rows: int = 2048) -> Solve:
+    """Whole solve of a GENERATED input without holding it (orc_similarity_
+    transform_gen_*): each round regenerates A_0 in row blocks and re-applies
+    the recorded transforms.  Bit-identical to similarity_transform() on the
+    same matrix; for the sizes that do not fit the host twice (configs[3]).
+    ``max_itr`` also bounds the row-sum history kept (max_itr * n)."""
+    sfx = _sfx(dtype)
+    T = np.dtype(dtype).type
+    if eps is None:
+        eps = EPS_F32 if T is np.float32 else EPS_F64
+    ev = np.zeros(1, dtype=dtype)
+    vec = np.zeros(n, dtype=dtype)
+    it = np.zeros(1, dtype=np.uint32)
+    ms = np.zeros(1, dtype=np.float64)
+    ev_n = np.zeros(1, dtype=np.uint32)
+    k = {"hilbert": 1, "random": 2}[kind]
+    rc = getattr(lib(), f"orc_similarity_transform_gen_{sfx}")(
+        k, seed, n, T(eps), max_itr, semantics, nthreads, chunk_rows,
+        _ptr(ev), _ptr(vec), _ptr(it), _ptr(ms), _ptr(ev_n))
+    if rc != 0:
+        raise ValueError("oracle generated solve failed (bad arguments or out of memory)")
+    return Solve(ev[0], vec, int(it[0]), int(ev_n[0]), float(ms[0]),
+                 np.zeros(0, dtype=np.float64))

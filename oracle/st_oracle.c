@@ -297,6 +297,77 @@ orc_now_ms(void)
     return 0;                                                                 \
   }
 
+/*
+ * Streaming form of the same loop for a GENERATED input too large to keep
+ * twice on the host (configs[3]: 65536^2 fp64 = 32 GiB): A_0 is never
+ * stored; round k regenerates it in blocks of chunk_rows rows, re-applies the
+ * k recorded transforms row by row with exactly orc_compute_next's
+ * operations, (1/s_i[r]) then x*(inv*s_i[c]) (or (inv*x)*s_i[c]), oldest
+ * first, and sums each row with orc_pairwise_sum.  Every element sees the
+ * same operations in the same order as in orc_similarity_transform and a
+ * row's sum depends on that row only, so the results are bit-identical to
+ * it (checked in tests/test_oracle.py); the cost is O(k) passes in round k,
+ * fine for the few rounds random inputs take.  kind 1 = Hilbert, 2 =
+ * seeded random.  max_itr bounds the s history (max_itr * n elements).
+ */
+#define DEFINE_SOLVE_GEN(T, SFX)                                              \
+  int orc_similarity_transform_gen_##SFX(                                     \
+    int kind, uint64_t seed, uint32_t n, T eps, uint32_t max_itr,             \
+    int semantics, int nthreads, uint32_t chunk_rows, T* eigen_val,           \
+    T* eigen_vec, uint32_t* iter_count, double* loop_ms,                      \
+    uint32_t* rounds_evaluated)                                               \
+  {                                                                           \
+    if (n == 0 || max_itr == 0 || (kind != 1 && kind != 2) || !eigen_val ||   \
+        !eigen_vec || !iter_count)                                            \
+      return -1;                                                              \
+    if (nthreads > 0)                                                         \
+      omp_set_num_threads(nthreads);                                          \
+    if (chunk_rows == 0 || chunk_rows > n)                                    \
+      chunk_rows = n;                                                         \
+    T* hist = (T*)malloc(sizeof(T) * (size_t)max_itr * n); /* s_0..s_k */     \
+    T* blk = (T*)malloc(sizeof(T) * (size_t)chunk_rows * n);                  \
+    if (!hist || !blk) {                                                      \
+      free(hist);                                                             \
+      free(blk);                                                              \
+      return -1;                                                              \
+    }                                                                         \
+    const int cyclic = semantics == ORC_SEM_SYCL;                             \
+    const int order = semantics == ORC_SEM_SYCL ? 0 : 1;                      \
+    for (uint32_t i = 0; i < n; i++)                                          \
+      eigen_vec[i] = (T)1;                                                    \
+    double t0 = orc_now_ms();                                                 \
+    uint32_t i = 0, evals = 0;                                                \
+    for (; i < max_itr; i++) {                                                \
+      T* s = hist + (size_t)i * n;                                            \
+      for (uint32_t r0 = 0; r0 < n; r0 += chunk_rows) {                       \
+        const uint32_t nr = n - r0 < chunk_rows ? n - r0 : chunk_rows;        \
+        if (kind == 1)                                                        \
+          orc_hilbert_##SFX(blk, nr, n, r0);                                  \
+        else                                                                  \
+          orc_random_##SFX(blk, nr, n, r0, seed);                             \
+        for (uint32_t j = 0; j < i; j++)                                      \
+          orc_compute_next_##SFX(blk, hist + (size_t)j * n, nr, n, r0,        \
+                                 order);                                      \
+        orc_rowsum_##SFX(blk, s + r0, nr, n);                                 \
+      }                                                                       \
+      evals++;                                                                \
+      T mx = orc_find_max_##SFX(s, n);                                        \
+      orc_compute_eigen_vector_##SFX(s, mx, eigen_vec, n);                    \
+      *eigen_val = s[0];                                                      \
+      if (orc_stop_##SFX(s, n, eps, cyclic))                                  \
+        break;                                                                \
+    }                                                                         \
+    double t1 = orc_now_ms();                                                 \
+    *iter_count = semantics == ORC_SEM_SYCL ? i : (i < max_itr ? i + 1 : i);  \
+    if (loop_ms)                                                              \
+      *loop_ms = t1 - t0;                                                     \
+    if (rounds_evaluated)                                                     \
+      *rounds_evaluated = evals;                                              \
+    free(hist);                                                               \
+    free(blk);                                                                \
+    return 0;                                                                 \
+  }
+
 #ifndef _OPENMP
 static void
 omp_set_num_threads(int n)
@@ -307,6 +378,8 @@ omp_set_num_threads(int n)
 
 DEFINE_SOLVE(double, f64)
 DEFINE_SOLVE(float, f32)
+DEFINE_SOLVE_GEN(double, f64)
+DEFINE_SOLVE_GEN(float, f32)
 
 int
 orc_max_threads(void)

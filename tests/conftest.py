@@ -55,3 +55,16 @@ def large_pin(n, dtype, seed=0):
         if (c["n"], c["dtype"], c["seed"]) == (n, dtype, seed):
             return c
     raise KeyError((n, dtype, seed))
+
+
+def large_oracle(name):
+    """The oracle's reference-semantics solve of a full-size seeded random
+    input (tests/golden/large_oracle.json + large_oracle_v.npz,
+    make_large_oracle.py): (case dict, eigenvector)."""
+    import json
+
+    import numpy as np
+    here = os.path.join(REPO, "tests", "golden")
+    doc = json.load(open(os.path.join(here, "large_oracle.json")))
+    with np.load(os.path.join(here, "large_oracle_v.npz")) as z:
+        return doc["cases"][name], z[name]

@@ -62,3 +62,48 @@ def test_bench_json_contract():
     assert c["kind"] in ("port", "reference") and c["value"] > 0
     # the reference-semantics solve inside the bench converged as published
     assert d["solve"]["iter_count"] == 17
+    assert c["affinity_cpus"] >= c["cores"] >= 1 and "cpu_model" in c
+    assert c["traffic_rate_3pass"] > c["value"]
+
+
+def test_one_gpu_lines_drop_fractions():
+    d = {"roofline": {"frac": 0.5, "achieved": 1.0}, "legs": [{"frac": 0.1, "x": 2}],
+         "north_star": {"target_frac": 0.7, "frac": 0.8}}
+    assert bench.strip_fracs(d) == {"roofline": {"achieved": 1.0}, "legs": [{"x": 2}],
+                                    "north_star": {}}
+
+
+def test_self_spawned_ranks_report_failure():
+    """`bench.py --gpus 2` without a launcher starts its two ranks itself and
+    exits with their status: here (no GPU) both ranks fail at set_device, so
+    the parent must fail too, promptly, and print no JSON line."""
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--no-cpu"], capture_output=True, text=True, timeout=300, cwd=REPO,
+                         env={k: v for k, v in os.environ.items()
+                              if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert out.returncode != 0
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_bench_self_spawned_two_ranks_on_one_gpu():
+    """The N > 1 line without torch.distributed.run: two self-spawned ranks
+    sharing cuda:0 over gloo carry the configs[3] strong-scaling leg (65536^2
+    fp64, 32768 rows per rank) checked against the oracle's solve, and are
+    marked non-representative (no roofline fractions)."""
+    out = subprocess.run(
+        [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--one-gpu",
+         "--backend", "gloo", "--steps", "5", "--warmup", "1", "--no-overlap-leg"],
+        capture_output=True, text=True, timeout=600, cwd=REPO,
+        env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["representative"] is False
+    assert "frac" not in d["roofline"]
+    c3 = d["configs3_strong"]
+    assert c3["n"] == 65536 and c3["rows_per_gpu"] == 32768 and "frac" not in c3
+    assert c3["solve"]["check"]["iter_count_equal"] is True
+    assert c3["solve"]["check"]["eigen_val_rel_err_vs_oracle"] <= 1e-10
+    assert d["exchange"]["backend"] == "gloo" and d["rccl_ranks"] is None

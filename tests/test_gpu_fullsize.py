@@ -1,0 +1,208 @@
+"""GPU parity at the BASELINE full sizes against the CPU oracle (not only
+through size-independent properties), and the multi-device paths at every
+device count the box has.
+
+Tolerances (as tests/test_gpu_parity.py):
+  * fp64 vs the oracle's same-semantics solve: iteration count equal, λ
+    relative <= 1e-10, eigenvector max-abs <= 1e-10 (the GPU sums rows in a
+    fixed tree, the oracle in numpy's pairwise order);
+  * fp32: iteration count equal, λ relative <= 1e-5, eigenvector max-abs
+    <= 1e-5 (fp32 row sums of ~16384 carry ulps of 2^-9).
+
+The oracle runs on the box's host cores inside the test where the input fits
+the host twice (32768², 8 GiB fp64 / 4 GiB fp32) and must reproduce the
+committed pins (tests/golden/large_oracle.json, make_large_oracle.py) bit
+for bit; 65536² (32 GiB) is checked against the committed pin only.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no HIP device", allow_module_level=True)
+
+from eigen_value_amd import _lib  # noqa: E402
+from eigen_value_amd import device as dev  # noqa: E402
+from conftest import large_oracle, large_pin  # noqa: E402
+
+DEV = "cuda:0"
+NDEV = torch.cuda.device_count()
+HOST_THREADS = len(os.sched_getaffinity(0))
+
+
+@pytest.fixture(scope="module")
+def solver():
+    s = dev.DeviceSolver(DEV)
+    yield s
+    s.close()
+
+
+def _free():
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def _host_oracle(orc, name, n, npdt, max_itr):
+    """The oracle's SYCL-semantics solve of the seeded input on this host,
+    checked bit for bit against the committed pin."""
+    mat = orc.generate_c("random", n, 0, npdt)
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL, max_itr=max_itr, nthreads=HOST_THREADS)
+    del mat
+    pin, v_pin = large_oracle(name)
+    assert (ref.iter_count, ref.rounds_evaluated) == (pin["iter_count"], pin["rounds_evaluated"])
+    assert float(ref.eigen_val) == pin["eigen_val"]
+    assert np.array_equal(ref.eigen_vec, v_pin)
+    return ref
+
+
+def test_config2_random32768_f64_vs_oracle(solver, orc):
+    """configs[2]: 32768² random fp64 (seed 0), the library's solve loop
+    (deferred writes), against the oracle's solve of the same matrix run on
+    the host (similarity_transform.cpp:39-53, stop :413-421, count :54)."""
+    n = 32768
+    ref = _host_oracle(orc, "random32768_f64", n, np.float64, 1000)
+    a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
+    lam, v, it, st = solver.solve(a, inplace=True)
+    assert it == ref.iter_count == 3 and st["rounds"] == ref.rounds_evaluated
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v.cpu().numpy() - ref.eigen_vec)) <= 1e-10
+    # the matrix-free form on a fresh copy of the input
+    dev.generate("random", n, torch.float64, seed=0, device=DEV, out=a)
+    lam_mf, v_mf, it_mf, _ = solver.solve(a, matrix_free=True)
+    assert it_mf == ref.iter_count
+    assert abs(lam_mf - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v_mf.cpu().numpy() - ref.eigen_vec)) <= 1e-10
+    del a, v, v_mf
+    _free()
+
+
+def test_config4_random32768_f32_vs_oracle(solver, orc):
+    """configs[4]: 32768² random fp32 over 8 rounds at the reference's
+    EPS = 1e-3f (the fp32 iteration does not stop at this size, so both
+    exhaust max_itr = 8) against the oracle's fp32 solve run on the host."""
+    n = 32768
+    ref = _host_oracle(orc, "random32768_f32_8rounds", n, np.float32, 8)
+    a = dev.generate("random", n, torch.float32, seed=0, device=DEV)
+    lam, v, it, st = solver.solve(a, inplace=True, max_itr=8)
+    assert it == ref.iter_count == 8 and st["rounds"] == 8 and st["converged"] == 0
+    assert abs(float(lam) - float(ref.eigen_val)) <= 1e-5 * float(ref.eigen_val)
+    assert np.max(np.abs(v.cpu().numpy().astype(np.float64) - ref.eigen_vec)) <= 1e-5
+    del a, v
+    _free()
+
+
+def test_config3_sharded_p1_vs_oracle():
+    """configs[3] size, 65536² random fp64 (32 GiB), through the row-block
+    driver (ShardedSimilarityTransform, P = 1: no process group, the block is
+    the whole matrix) with its default deferred-write solve, against the
+    oracle's solve of the same matrix (committed pin: the streaming oracle,
+    bit-identical to the plain loop) and the true Perron root."""
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+    pin, v_pin = large_oracle("random65536_f64")
+    n = 65536
+    sh = ShardedSimilarityTransform(n, torch.float64)
+    assert sh.part.nrows == n and sh.deferred_writes
+    sh.load("random", seed=0)
+    lam, v, it, rounds = sh.solve()
+    assert it == pin["iter_count"] == 3 and rounds == pin["rounds_evaluated"]
+    assert abs(lam - pin["eigen_val"]) <= 1e-10 * pin["eigen_val"]
+    assert np.max(np.abs(v.cpu().numpy() - v_pin)) <= 1e-10
+    perron = large_pin(n, "f64")["lambda"]
+    assert abs(lam - perron) / perron < 1e-6
+    sh.close()
+    del sh, v
+    _free()
+
+
+# ---------------------------------------------------------------------------
+# every device the box has (8 on the driver's node, 1 here)
+# ---------------------------------------------------------------------------
+def _device_counts():
+    if NDEV > 1:
+        return [1, NDEV]
+    return [1, pytest.param(2, id="ngpus2-skipped-needs-2-devices",
+                            marks=pytest.mark.skip(reason=f"needs >= 2 HIP devices, "
+                                                          f"this box has {NDEV}"))]
+
+
+@pytest.mark.parametrize("ngpus", _device_counts())
+def test_native_multi_gpu_all_devices(orc, ngpus):
+    """st_solve_multi_* over `ngpus` devices (ncclCommInitAll, one all-gather
+    per round) vs the oracle: a k_round block size and a flat-round
+    (deferred-write) block size."""
+    from eigen_value_amd.multi import solve_multi
+    for n in (3001, 9216 * max(1, ngpus // 2)):
+        mat = orc.random_matrix(n, 3) if n <= 12000 else orc.generate_c("random", n, 3)
+        ref = orc.similarity_transform(mat, orc.SEM_SYCL, nthreads=HOST_THREADS)
+        del mat
+        lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=3)
+        assert it == ref.iter_count and st["rounds"] == ref.rounds_evaluated, n
+        assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+        assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
+        r2 = solve_multi(n, "random", ngpus=ngpus, seed=3, write_every_round=True)
+        assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
+
+
+def _comm_worker(rank, world, port, outdir):
+    import torch.distributed as dist
+    from eigen_value_amd.sharded import RcclComm, ShardedSimilarityTransform
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", rank))
+    try:
+        rc = RcclComm()
+        info = rc.info()
+        for dt in (torch.float64, torch.float32):
+            out = torch.full((world * 5,), -1.0, dtype=dt, device="cuda")
+            out[rank * 5:(rank + 1) * 5] = torch.arange(rank * 5, rank * 5 + 5, dtype=dt)
+            rc.allgather(out, out[rank * 5:(rank + 1) * 5])
+            torch.cuda.synchronize()
+            assert torch.equal(out.cpu(), torch.arange(world * 5, dtype=dt))
+        rc.close()
+        res = []
+        for n in (3001, 9216):       # k_round and flat (deferred) blocks
+            sh = ShardedSimilarityTransform(n, torch.float64, comm="native")
+            assert sh.rccl is not None
+            sh.load("random", seed=3)
+            lam, v, it, rounds = sh.solve()
+            sh.close()
+            res += [lam, it, rounds]
+            if rank == 0:
+                np.save(os.path.join(outdir, f"v{n}.npy"), v.cpu().numpy())
+        np.save(os.path.join(outdir, f"r{rank}.npy"),
+                np.array([info["nranks"], info["rank"], info["device"], *res]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [NDEV] if NDEV > 1 else [
+    pytest.param(2, id="world2-skipped-needs-2-devices",
+                 marks=pytest.mark.skip(reason=f"RCCL needs one device per rank; "
+                                               f"this box has {NDEV}"))])
+def test_library_comm_all_devices(tmp_path, orc, world):
+    """The library-owned RCCL communicator (st_comm_*) with nranks = every
+    device: RCCL reports that many ranks, the in-slot all-gather is right,
+    and the one-process-per-GPU sharded solve matches the oracle."""
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    mp.spawn(_comm_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        got = np.load(tmp_path / f"r{r}.npy")
+        assert tuple(int(x) for x in got[:3]) == (world, r, r)
+        for j, n in enumerate((3001, 9216)):
+            ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL,
+                                           nthreads=HOST_THREADS)
+            lam, it, rounds = got[3 + 3 * j:6 + 3 * j]
+            assert int(it) == ref.iter_count and int(rounds) == ref.rounds_evaluated
+            assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+            if r == 0:
+                v = np.load(tmp_path / f"v{n}.npy")
+                assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10

@@ -761,8 +761,10 @@ def test_fp32_large_never_converges_at_reference_eps(solver):
 
 def test_config4_size_on_one_gpu(solver):
     """BASELINE configs[3] size, 65536² fp64 = 32 GiB (N² = 2^32 elements:
-    exercises every 64-bit index path), on one GPU: converges, residual
-    small, matrix-free agrees, and the 32 GiB row-block path with P = 1."""
+    exercises every 64-bit index path), on one GPU through DeviceSolver:
+    converges, residual small, matrix-free agrees.  The row-block driver at
+    P = 1 on the same size, against the oracle's solve, is
+    test_gpu_fullsize.py::test_config3_sharded_p1_vs_oracle."""
     n = 65536
     a = dev.generate("random", n, torch.float64, seed=0, device=DEV)
     lam_mf, v_mf, it_mf, _ = solver.solve(a, matrix_free=True)
@@ -813,6 +815,7 @@ def _rccl_worker(rank, port, outdir):
         # the library-owned communicator (id broadcast over the group)
         from eigen_value_amd.sharded import RcclComm
         rc = RcclComm()
+        assert rc.info() == {"nranks": 1, "rank": 0, "device": 0}
         for dt in (torch.float64, torch.float32):
             out = torch.arange(12, dtype=dt, device="cuda")
             rc.allgather(out, out[0:12])

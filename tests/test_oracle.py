@@ -171,3 +171,26 @@ def test_large_pins(orc):
             getattr(orc.lib(), f"orc_random_{dt}")(c.ctypes.data_as(ctypes.c_void_p), 1, n, row0, 0)
             ref = orc.random_matrix(n, 0, npdt, nrows=1, row0=row0)
             assert np.array_equal(c, ref)
+
+
+@pytest.mark.parametrize("kind,n,dtype,semantics,eps,max_itr", [
+    ("random", 1000, np.float64, 0, None, 64),
+    ("hilbert", 777, np.float64, 1, None, 64),
+    ("hilbert", 1024, np.float32, 0, None, 64),
+    ("random", 2000, np.float64, 1, 0.0, 5),
+    ("random", 513, np.float32, 0, 0.0, 8),
+])
+def test_generated_solve_bit_identical(orc, kind, n, dtype, semantics, eps, max_itr):
+    """The streaming oracle for generated inputs too large to hold twice
+    (orc_similarity_transform_gen_*: A_0 regenerated in row blocks each round,
+    recorded transforms re-applied) equals the plain oracle loop bit for bit;
+    it produces the configs[3] pins (tests/golden/make_large_pins.py)."""
+    a = orc.generate_c(kind, n, 3, dtype)
+    ref = orc.hilbert(n, dtype) if kind == "hilbert" else orc.random_matrix(n, 3, dtype)
+    assert np.array_equal(a, ref)
+    r1 = orc.similarity_transform(a, semantics, eps=eps, max_itr=max_itr)
+    r2 = orc.similarity_transform_gen(kind, n, 3, dtype, semantics, eps=eps,
+                                      max_itr=max_itr, chunk_rows=97)
+    assert (r1.iter_count, r1.rounds_evaluated) == (r2.iter_count, r2.rounds_evaluated)
+    assert r1.eigen_val == r2.eigen_val
+    assert np.array_equal(r1.eigen_vec, r2.eigen_vec)

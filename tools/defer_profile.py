@@ -1,72 +1,108 @@
 #!/usr/bin/env python3
-"""Fixed-round device solves with and without deferred writes, for
-rocprofv3 kernel traces and PMC passes of the deferred flat round.
+"""The deferred-write flat round (the solve loops' form for blocks of >= 144
+MiB) over whole store cycles, for rocprofv3 kernel traces and PMC passes,
+with HIP-event timing of the same launches.
 
-    rocprofv3 --kernel-trace --stats -d OUT -o run -- python3 tools/defer_profile.py
-    python3 tools/defer_profile.py --trace OUT/run_kernel_trace.csv   # summarise
+    rocprofv3 --kernel-trace --stats -d OUT -o run -- \\
+        python3 tools/defer_profile.py --kind random --n 32768 --events OUT/events.json
+    python3 tools/defer_profile.py --kind random --n 32768 \\
+        --trace OUT/run_kernel_trace.csv --events OUT/events.json --json OUT/cycle.json
 
-One solve of --rounds rounds (eps = 0) per mode on an --n x --n random
-matrix (fp64 by default), so the trace holds the deferred k_flat launches
-(last template argument NP = 0, 1, 2: the pending rounds each re-applies;
-NP = 2 also stores) next to the every-round ones (NP = -1).
+Run mode: ShardedSimilarityTransform at P = 1 (the same st_round_flat_
+deferred launches as DeviceSolver's solve loop) runs 2 warm-up cycles, then
+--cycles store cycles of m rounds (bench.py timed_deferred: the first round
+after a store ... the storing round, no flush), timed with HIP events; the
+per-round figure goes to --events.  Summary mode reads the kernel trace:
+k_flat launches by their last template argument NP (the pending rounds a
+launch re-applies; NP = m - 1 also stores; -1 = stores every round) and the
+k_parts launch that follows each, and writes per-NP averages and their sum
+over one cycle per round (`cycle_ms_per_round`) next to the events' figure
+(--json: profiles/rNN_defer_cycle_<workload>.json, read by bench.py).
 """
 import argparse
 import csv
+import json
 import os
+import re
 import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
+def rounds_per_store(n, elem, f64):
+    # st_defer_rounds: 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32
+    return 4 if n * n * elem >= 2 << 30 else (3 if f64 else 4)
+
+
 def run(args):
     import torch
-    from eigen_value_amd import device as dev
+    import bench
+    from eigen_value_amd import sharded
     dt = torch.float64 if args.dtype == "f64" else torch.float32
-    a0 = dev.generate("random", args.n, dt, seed=0, device="cuda:0")
-    solver = dev.DeviceSolver("cuda:0")
-    out = {}
-    for every in (False, True):
-        a = a0.clone()
-        lam, v, it, st = solver.solve(a, inplace=True, eps=0.0, max_itr=args.rounds,
-                                      write_every_round=every)
-        torch.cuda.synchronize()
-        out[every] = (lam, v.cpu(), a)
-        print(f"write_every_round={every}: {it} rounds, lambda={lam!r}, "
-              f"loop {st['loop_ms']:.3f} ms", flush=True)
-    same = out[False][0] == out[True][0] and torch.equal(out[False][1], out[True][1]) \
-        and torch.equal(out[False][2], out[True][2])
-    print(f"bitwise equal (lambda, v, final matrix): {same}", flush=True)
-    solver.close()
+    sh = sharded.ShardedSimilarityTransform(args.n, dt)
+    assert sh.deferred_writes, "block below the flat-round size: no deferred writes"
+    sh.load(args.kind, seed=0)
+    el, ev_ms, m = bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)
+    out = {"workload": f"{args.kind}{args.n}_{args.dtype}", "m": m, "cycles": args.cycles,
+           "event_ms_per_round": ev_ms, "host_ms_per_round": el / (args.cycles * m) * 1e3}
+    print(json.dumps(out), flush=True)
+    if args.events:
+        json.dump(out, open(args.events, "w"), indent=1)
+    sh.close()
 
 
 def np_of(name):
     """k_flat's last template argument: -1 = stores every round, else the
     number of pending rounds it re-applies (its position in the group)."""
-    import re
     m = re.search(r"k_flat<([^>]*)>", name)
     return int(m.group(1).split(",")[11])
 
 
-def summarise(path, n, elem, m=3):
-    rows = [r for r in csv.DictReader(open(path)) if "k_flat<" in r["Kernel_Name"]]
-    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6
+def summarise(path, n, elem, m, workload, events=None):
+    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # noqa: E731
+    flat, parts, last = {}, {}, None
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "k_flat<" in name:
+            last = np_of(name)
+            flat.setdefault(last, []).append(dur(r))
+        elif "k_parts<" in name and last is not None:
+            parts.setdefault(last, []).append(dur(r))
+            last = None
     nb = n * n * elem
-    every = [dur(r) for r in rows if np_of(r["Kernel_Name"]) < 0]
-    if every:
-        t = sum(every) / len(every)
-        print(f"every-round k_flat: {len(every)} launches, avg {t:.4f} ms "
-              f"({2 * nb / (t * 1e-3) / 1e9:.0f} GB/s on 2 N^2 b)")
-    for pos in range(m):
-        g = [dur(r) for r in rows if np_of(r["Kernel_Name"]) == pos]
-        if g:
-            t = sum(g) / len(g)
-            b = (2 if pos == m - 1 else 1) * nb
-            print(f"deferred k_flat, {pos} pending ({'read + write' if pos == m - 1 else 'read only'}):"
-                  f" {len(g)} launches, avg {t:.4f} ms ({b / (t * 1e-3) / 1e9:.0f} GB/s)")
+    avg = lambda x: sum(x) / len(x)  # noqa: E731
+    out = {"workload": workload, "m": m, "trace": path, "k_flat": {}, "k_parts": {}}
+    for pos in sorted(flat):
+        t = avg(flat[pos])
+        b = 2 * nb if pos in (-1, m - 1) else nb
+        out["k_flat"][str(pos)] = {"launches": len(flat[pos]), "avg_ms": round(t, 5),
+                                   "bytes": b, "GBs": round(b / (t * 1e-3) / 1e9, 1)}
+        if pos in parts:
+            out["k_parts"][str(pos)] = round(avg(parts[pos]), 5)
+        print(f"k_flat NP={pos}: {len(flat[pos])} launches, avg {t:.4f} ms "
+              f"({b / (t * 1e-3) / 1e9:.0f} GB/s)" + (
+                  f", k_parts {avg(parts[pos]):.4f} ms" if pos in parts else ""))
+    if all(p in flat and p in parts for p in range(m)):
+        cyc = sum(avg(flat[p]) + avg(parts[p]) for p in range(m)) / m
+        out["cycle_ms_per_round"] = round(cyc, 5)
+        by = (m + 1.0) / m * nb
+        out["cycle_GBs"] = round(by / (cyc * 1e-3) / 1e9, 1)
+        print(f"one store cycle: {cyc:.4f} ms per round ({out['cycle_GBs']:.0f} GB/s on "
+              f"(m+1)/m N^2 b)")
+    if events:
+        ev = json.load(open(events))
+        out["event_ms_per_round"] = round(ev["event_ms_per_round"], 5)
+        if "cycle_ms_per_round" in out:
+            out["events_over_rocprof"] = round(ev["event_ms_per_round"]
+                                               / out["cycle_ms_per_round"], 4)
+            print(f"HIP events: {ev['event_ms_per_round']:.4f} ms per round "
+                  f"(x{out['events_over_rocprof']:.4f} the rocprof cycle sum)")
+    return out
 
 
-def summarise_pmc(fetch, write, n, elem, m=3):
+def summarise_pmc(fetch, write, n, elem, m):
     """HBM bytes per deferred k_flat launch by pending count: 2*FETCH_SIZE
     (the gfx950 wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE,
     KiB counters, from separate passes."""
@@ -80,31 +116,42 @@ def summarise_pmc(fetch, write, n, elem, m=3):
 
     f, w = per_pos(fetch), per_pos(write)
     nb = n * n * elem
+    res = {}
     for pos in sorted(f):
         if pos in w:
             rd, wr = 2 * sum(f[pos]) / len(f[pos]), sum(w[pos]) / len(w[pos])
             alg = (2 if pos == m - 1 else 1) * nb
+            res[str(pos)] = {"read": rd, "write": wr, "algorithmic": alg,
+                             "ratio": round((rd + wr) / alg, 4)}
             print(f"deferred k_flat, {pos} pending: read {rd / 1e9:.3f} GB, "
                   f"write {wr / 1e9:.3f} GB per launch; algorithmic {alg / 1e9:.3f} GB "
                   f"(x{(rd + wr) / alg:.4f})")
+    return res
 
 
 if __name__ == "__main__":
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=32768)
-    p.add_argument("--rounds", type=int, default=30)
+    p.add_argument("--kind", default="random", choices=["hilbert", "random"])
+    p.add_argument("--cycles", type=int, default=8)
     p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
+    p.add_argument("--events", help="run mode: write the HIP-event figure here; summary "
+                                    "mode: read it")
     p.add_argument("--trace", help="summarise a rocprofv3 kernel trace instead of running")
+    p.add_argument("--json", help="summary mode: write the summary here")
     p.add_argument("--fetch", help="with --write: summarise FETCH_SIZE / WRITE_SIZE passes")
     p.add_argument("--write")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
-    # rounds per store (st_defer_rounds): 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32
-    m = 4 if a.n * a.n * elem >= 2 << 30 else (3 if a.dtype == "f64" else 4)
+    m = rounds_per_store(a.n, elem, a.dtype == "f64")
+    wl = f"{a.kind}{a.n}_{a.dtype}"
     if a.trace or a.fetch:
+        res = {}
         if a.trace:
-            summarise(a.trace, a.n, elem, m)
+            res = summarise(a.trace, a.n, elem, m, wl, a.events)
         if a.fetch and a.write:
-            summarise_pmc(a.fetch, a.write, a.n, elem, m)
+            res["pmc"] = summarise_pmc(a.fetch, a.write, a.n, elem, m)
+        if a.json:
+            json.dump(res, open(a.json, "w"), indent=1)
     else:
         run(a)

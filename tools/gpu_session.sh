@@ -32,7 +32,7 @@ nproc > "$OUT/host.txt"; lscpu | grep -E 'Model name|^CPU\(s\)' >> "$OUT/host.tx
 
 for s in $STEPS; do
   case $s in
-    tests) step pytest_gpu 1200 python -m pytest tests -m gpu -x -q -rA ;;
+    tests) step pytest_gpu 1200 python -u -m pytest tests -m gpu -x -v -rA --timeout 300 --timeout-method thread ;;
     smoke) step smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
     bench) step bench 600 python bench.py ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --no-cpu ;;
@@ -57,6 +57,20 @@ for s in $STEPS; do
     overlap) # the overlapped exchange: N = 1 (split launches, empty gather) and the rehearsal
       step bench_overlap_p1 600 python bench.py --overlap --no-cpu --no-north-star --no-headline
       step bench_overlap_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu --overlap --no-overlap-leg ;;
+    spawn) # the N > 1 line without a launcher: two self-spawned ranks on one GPU (gloo)
+      step bench_spawn_p2 900 python bench.py --gpus 2 --one-gpu --backend gloo --steps 20 --warmup 3 --no-overlap-leg ;;
+    defer) # the deferred-write rounds over whole store cycles: rocprof + HIP events
+      for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
+        set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_${K}${N}_${DT}"; mkdir -p "$D"
+        step "defer_${K}${N}_${DT}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --events "$D/events.json"
+        python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --trace "$D/prof/run_kernel_trace.csv" --events "$D/events.json" --json "$D/cycle.json" | tee -a "$OUT/session.log"
+      done ;;
+    profile_f32) # configs[4]: 32768^2 fp32 every-round flat round, trace + PMC passes
+      D="$OUT/random32768_f32"
+      step prof_f32 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind random --n 32768 --dtype f32 --steps 50 --warmup 3 --no-cpu --no-north-star --no-headline
+      step pmc_fetch_f32 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 bench.py --kind random --n 32768 --dtype f32 --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
+      step pmc_write_f32 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 bench.py --kind random --n 32768 --dtype f32 --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
+      python3 tools/pmc_traffic.py --workload random32768_f32 --n 32768 --elem 4 --dtype float --fetch "$D/pmc_fetch/run_counter_collection.csv" --write "$D/pmc_write/run_counter_collection.csv" --trace "$D/prof/run_kernel_trace.csv" --out "$D/pmc.json" | tee -a "$OUT/session.log" ;;
     split) step split_cost 600 python3 tools/split_cost.py ;;
     fp32)  step fp32_study 600 python3 tools/fp32_study.py --out "$OUT/fp32_study.json" ;;
     profile)
