@@ -206,7 +206,28 @@ def cw_bound(torch, a0, v, lam):
     return max(abs(lam - lo), abs(lam - hi)) / abs(lam)
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the cgroup grants this process (cpu.max on v2,
+    cpu.cfs_quota_us / cpu.cfs_period_us on v1), or None if unlimited."""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def host_info() -> dict:
+    """The host the CPU baseline runs on.  `threads` = every CPU this
+    process may actually use: the affinity mask, bounded by the cgroup's
+    CPU quota and by OMP_NUM_THREADS when the environment sets it (the GPU
+    box's lease exposes all 256 CPUs in the mask but grants a 16-CPU share:
+    256 OpenMP threads there ran 55x slower than 16)."""
     model = None
     try:
         for ln in open("/proc/cpuinfo"):
@@ -215,8 +236,16 @@ def host_info() -> dict:
                 break
     except OSError:
         pass
-    return {"cpu_model": model, "nproc": os.cpu_count(),
-            "affinity_cpus": len(os.sched_getaffinity(0))}
+    aff = len(os.sched_getaffinity(0))
+    quota = cgroup_cpu_quota()
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = aff
+    if quota is not None:
+        threads = min(threads, max(1, int(math.ceil(quota))))
+    if omp and omp.isdigit() and int(omp) > 0:
+        threads = min(threads, int(omp))
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff,
+            "cgroup_cpu_quota": quota, "omp_num_threads": omp, "threads": threads}
 
 
 # ---------------------------------------------------------------------------
@@ -502,7 +531,7 @@ def cpu_leg(args, np_, workload, n, bytes_round_total, ms_per_step):
     sample BASELINE.md §3 plans."""
     from oracle import oracle as orc
     info = host_info()
-    threads = info["affinity_cpus"]
+    threads = info["threads"]
     b = 8 if args.dtype == "f64" else 4
     npdt = np_.float64 if args.dtype == "f64" else np_.float32
     mat = orc.generate_c(args.kind, n, 0, npdt)

@@ -68,3 +68,10 @@ def large_oracle(name):
     doc = json.load(open(os.path.join(here, "large_oracle.json")))
     with np.load(os.path.join(here, "large_oracle_v.npz")) as z:
         return doc["cases"][name], z[name]
+
+
+def host_threads() -> int:
+    """CPUs the oracle may use on this host: the affinity mask bounded by the
+    cgroup quota and OMP_NUM_THREADS (bench.host_info)."""
+    import bench
+    return bench.host_info()["threads"]

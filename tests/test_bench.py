@@ -62,7 +62,7 @@ def test_bench_json_contract():
     assert c["kind"] in ("port", "reference") and c["value"] > 0
     # the reference-semantics solve inside the bench converged as published
     assert d["solve"]["iter_count"] == 17
-    assert c["affinity_cpus"] >= c["cores"] >= 1 and "cpu_model" in c
+    assert c["affinity_cpus"] >= c["cores"] == c["threads"] >= 1 and "cpu_model" in c
     assert c["traffic_rate_3pass"] > c["value"]
 
 

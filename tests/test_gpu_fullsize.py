@@ -28,11 +28,11 @@ if not torch.cuda.is_available():
 
 from eigen_value_amd import _lib  # noqa: E402
 from eigen_value_amd import device as dev  # noqa: E402
-from conftest import large_oracle, large_pin  # noqa: E402
+from conftest import host_threads, large_oracle, large_pin  # noqa: E402
 
 DEV = "cuda:0"
 NDEV = torch.cuda.device_count()
-HOST_THREADS = len(os.sched_getaffinity(0))
+HOST_THREADS = host_threads()
 
 
 @pytest.fixture(scope="module")
