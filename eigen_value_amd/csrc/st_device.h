@@ -67,22 +67,33 @@ hsum(const typename vec<T, W>::type& y)
 }
 
 // DPP lane move (gfx9 data-parallel primitives; 64-bit values move as two
-// dwords).  Lanes outside ROW_MASK read 0.
+// dwords).  Lanes outside ROW_MASK receive an UNDEFINED value (mov_dpp: no
+// zero-initialised `old` operand, which cost two v_mov per 64-bit step -
+// 12 of the 30 VALU instructions of a double wave_sum): every reduction
+// below reads its result in lane 63 only, and lane 63's dependency chain
+// never passes through a masked-out lane (row_bcast 15 writes rows 1 and 3,
+// row_bcast 31 rows 2 and 3, and lane 63 sums lanes 31 and 47 from those).
+#ifndef ST_DPP_NOINIT
+#define ST_DPP_NOINIT 1
+#endif
 template <int CTRL, int ROW_MASK = 0xf, typename T>
 __device__ __forceinline__ T
 dpp_mov(T x)
 {
+#if ST_DPP_NOINIT
+#define ST_DPP32(v) __builtin_amdgcn_mov_dpp((v), CTRL, ROW_MASK, 0xf, false)
+#else
+#define ST_DPP32(v) __builtin_amdgcn_update_dpp(0, (v), CTRL, ROW_MASK, 0xf, false)
+#endif
   if constexpr (sizeof(T) == 4) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(
-      0, __float_as_int((float)x), CTRL, ROW_MASK, 0xf, false));
+    return __int_as_float(ST_DPP32(__float_as_int((float)x)));
   } else {
     const long long b = __double_as_longlong((double)x);
-    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, ROW_MASK, 0xf,
-                                               false);
-    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL,
-                                               ROW_MASK, 0xf, false);
+    const int lo = ST_DPP32((int)b);
+    const int hi = ST_DPP32((int)(b >> 32));
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
   }
+#undef ST_DPP32
 }
 
 template <typename T>
@@ -107,7 +118,7 @@ read_lane63(T x)
 // sum never depends on which kernel or partition computed it.
 template <typename T>
 __device__ __forceinline__ T
-wave_sum(T x)
+wave_sum_l63(T x) // the sum, valid in lane 63 only
 {
   x += dpp_mov<0xB1>(x);       // quad_perm [1,0,3,2]
   x += dpp_mov<0x4E>(x);       // quad_perm [2,3,0,1]
@@ -115,7 +126,63 @@ wave_sum(T x)
   x += dpp_mov<0x128>(x);      // row_ror 8
   x += dpp_mov<0x142, 0xa>(x); // row_bcast 15
   x += dpp_mov<0x143, 0xc>(x); // row_bcast 31
-  return read_lane63(x);
+  return x;
+}
+
+template <typename T>
+__device__ __forceinline__ T
+wave_sum(T x)
+{
+  return read_lane63(wave_sum_l63(x));
+}
+
+// x + (x of lane l ^ PL), PL = 16 (the same lane of the neighbouring row
+// of 16) or 32 (of the other half-wave), with the gfx950 permlane swaps:
+// swapping a value with itself leaves {own, partner} in the two results -
+// which one is which depends on the lane, and the sum does not
+template <int PL, typename T>
+__device__ __forceinline__ T
+permlane_add(T x)
+{
+  auto sw = [](int v) {
+    return PL == 16 ? __builtin_amdgcn_permlane16_swap(v, v, false, false)
+                    : __builtin_amdgcn_permlane32_swap(v, v, false, false);
+  };
+  if constexpr (sizeof(T) == 4) {
+    const auto r = sw(__float_as_int((float)x));
+    return __int_as_float((int)r[0]) + __int_as_float((int)r[1]);
+  } else {
+    const long long b = __double_as_longlong((double)x);
+    const auto lo = sw((int)b), hi = sw((int)(b >> 32));
+    const double a0 = __longlong_as_double(((long long)(int)hi[0] << 32) | (unsigned)lo[0]);
+    const double a1 = __longlong_as_double(((long long)(int)hi[1] << 32) | (unsigned)lo[1]);
+    return a0 + a1;
+  }
+}
+
+// Two rows' wave sums in one tree (rows x0, x1 of every lane): the first
+// step hands each lane of a pair the other's value of ONE row (even lanes
+// keep row 0, odd lanes row 1), the next three run wave_sum's DPP steps on
+// the interleaved rows (lane l ^ 2, ror 4, ror 8 keep a lane's parity), and
+// the last two add the same lane of the other row of 16 / half-wave
+// (permlane swaps keep the position).  Every addition is one of
+// wave_sum's, operands in the same pairs, so lane 62 ends with
+// wave_sum(x0) and lane 63 with wave_sum(x1), bit for bit, in 22 VALU
+// instructions for the two (fp64) instead of 36.
+template <typename T>
+__device__ __forceinline__ T
+wave_sum_pair(T x0, T x1)
+{
+  const bool odd = (threadIdx.x & 1u) != 0; // blocks are whole waves
+  const T keep = odd ? x1 : x0;
+  const T send = odd ? x0 : x1;
+  T x = keep + dpp_mov<0xB1>(send); // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);            // quad_perm [2,3,0,1]
+  x += dpp_mov<0x124>(x);           // row_ror 4
+  x += dpp_mov<0x128>(x);           // row_ror 8
+  x = permlane_add<16>(x);          // + the other row of 16
+  x = permlane_add<32>(x);          // + the other half-wave
+  return x;                         // lane 62: row 0, lane 63: row 1
 }
 
 // wave_sum of NR independent values, step by step across them (no stall
@@ -165,6 +232,37 @@ ld(const V* p)
     return __builtin_nontemporal_load(p);
   else
     return *p;
+}
+
+// A value every lane of the wave needs (a row's scale).  ST_ROW_VLOAD=1
+// loads it through the VECTOR memory path instead of a scalar load (whose
+// lgkmcnt wait - scalar loads return out of order, so a wave can only wait
+// for all of them - then also holds up the next kernel-argument pointer a
+// vector load needs).  Measured (tools/flat_map_sweep{,_vload},
+// profiles/r02_flat_map_rowload_*.log): 15-30 % SLOWER on non-temporal
+// fp64 blocks with pending rounds (32768^2, NP = 1: 1.62 vs 1.33 ms), equal
+// elsewhere, so the library keeps scalar row loads.
+#ifndef ST_ROW_VLOAD
+#define ST_ROW_VLOAD 0
+#endif
+// k_flat's unsplit rounds without load predicates (ST_FLAT_UNMASKED, see
+// k_flat); 0 keeps the predicated loads of the split rounds for them too
+#ifndef ST_FLAT_UNMASKED
+#define ST_FLAT_UNMASKED 1
+#endif
+template <typename T>
+__device__ __forceinline__ T
+ld_row(const T* p)
+{
+#if ST_ROW_VLOAD
+  // global (not flat: a flat load counts in lgkmcnt as well)
+  using GP = const __attribute__((address_space(1))) T*;
+  GP g = (GP)p;
+  asm volatile("" : "+v"(g));
+  return *g;
+#else
+  return *p;
+#endif
 }
 
 template <typename V, bool NT>
@@ -855,6 +953,8 @@ struct FlatPending
   const T* inv[NP > 0 ? NP : 1];
   const T* inv_cur; // 1 / s_k (the current round's row scales)
   uint32_t store;   // store A_{k+1} this round
+  uint32_t pt;      // piece-tiled workgroup order: pt row groups of a piece
+                    // back to back (0 = row-major; see k_flat)
 };
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
@@ -928,6 +1028,16 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       const uint32_t q = bb - (rg - 1) * pr;
       p = q < pa ? q : q + nfull;
     }
+  } else if (NP >= 0 && pend.pt != 0) {
+    // piece-tiled order (deferred rounds): pt row groups of one piece run
+    // back to back (the XCDs take every 8th), so the workgroups a CU runs
+    // in turn share the piece's column scales - s_k and the pending
+    // rounds' - in its L1 instead of refetching them from L2
+    const uint32_t pt = pend.pt, ng = (nrows + R - 1) / R;
+    const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
+    const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;
+    p = t / g;
+    rg = tile * pt + (t - p * g);
   } else {
     rg = b / ppr;
     p = b - rg * ppr;
@@ -944,27 +1054,43 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     in_cols[u] = c < ncols;
     in[u] = in_cols[u] && (SPLIT == 0 || ((c >= col0 && c < col1) == (SPLIT == 1)));
   }
+  // SPLIT == 0 loads without predicates: a row past the block reads the
+  // block's last row and a column chunk past ncols the last chunk (valid
+  // memory; their results are neither stored nor summed), so the element
+  // math below runs unmasked - no exec-mask branches around the loads, no
+  // v_cndmask per element and pending round
+  // (only rounds with pending scalings gain: 1-2 % at NP = 2, 3 on 32768^2
+  // fp64; the every-round and NP = 0 forms lose up to 3 %,
+  // profiles/r02_flat_map_ab_*.log)
+  constexpr bool UM = SPLIT == 0 && NP > 0 && ST_FLAT_UNMASKED;
+  uint32_t cl[U]; // the column each lane loads
+#pragma unroll
+  for (int u = 0; u < U; u++)
+    cl[u] = (!UM || in_cols[u]) ? c0 + u * BLK * W : ncols - W;
 #pragma unroll
   for (int j = 0; j < R; j++) {
     acc[j] = (T)0;
+    if constexpr (UM) {
+      const uint32_t rj = r0 + j < nrows ? r0 + j : nrows - 1; // uniform
 #pragma unroll
-    for (int u = 0; u < U; u++)
-      if (in[u] && r0 + j < nrows)
-        x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
-                                                 u * BLK * W));
-    // s_k[r], or with deferred writes already 1 / s_k[r]
-    const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
-    sr[j] = r0 + j < nrows ? rs[row0 + r0 + j] : (T)1;
+      for (int u = 0; u < U; u++)
+        x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)rj * ncols + cl[u]));
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+        if (in[u] && r0 + j < nrows)
+          x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
+                                                   u * BLK * W));
+    }
   }
   // the piece's column scales, issued with the matrix loads (the stats of
   // the first row group read them too)
   V sc[U];
 #pragma unroll
   for (int u = 0; u < U; u++)
-    if (in_cols[u])
-      sc[u] = *reinterpret_cast<const V*>(s_cur + c0 + u * BLK * W);
-  // deferred writes: the pending rounds' scales, issued with the matrix
-  // loads
+    if (UM || in_cols[u])
+      sc[u] = *reinterpret_cast<const V*>(s_cur + cl[u]);
+  // deferred writes: the pending rounds' column scales
   V sp_c[NP > 0 ? NP : 1][U];
   T sp_r[NP > 0 ? NP : 1][R]; // 1 / s_i[r]
   if constexpr (NP > 0) {
@@ -972,11 +1098,23 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     for (int i = 0; i < NP; i++) {
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (in_cols[u])
-          sp_c[i][u] = *reinterpret_cast<const V*>(pend.s[i] + c0 + u * BLK * W);
+        if (UM || in_cols[u])
+          sp_c[i][u] = *reinterpret_cast<const V*>(pend.s[i] + cl[u]);
+    }
+  }
+  // then the row scales (vector loads, ld_row): s_k[r], or with deferred
+  // writes already 1 / s_k[r], and the pending rounds' 1 / s_i[r]
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
+    sr[j] = r0 + j < nrows ? ld_row(rs + row0 + r0 + j) : (T)1;
+  }
+  if constexpr (NP > 0) {
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
 #pragma unroll
       for (int j = 0; j < R; j++)
-        sp_r[i][j] = r0 + j < nrows ? pend.inv[i][row0 + r0 + j] : (T)1;
+        sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
     }
   }
   if constexpr (GATE == kGateSpec) {
@@ -1008,7 +1146,38 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     }
   }
 #pragma unroll
-  for (int u = 0; u < U; u++) {
+  for (int u = 0; u < U && UM; u++) {
+    // unmasked (see the loads): every lane and row computes; the stores
+    // and the sums take the block's own elements only
+    if constexpr (NP > 0) {
+#pragma unroll
+      for (int i = 0; i < NP; i++) {
+#pragma unroll
+        for (int j = 0; j < R; j++) {
+          const T inv = sp_r[i][j];
+          if constexpr (ORDER == 0)
+            x[u][j] = x[u][j] * (inv * sp_c[i][u]);
+          else
+            x[u][j] = (inv * x[u][j]) * sp_c[i][u];
+        }
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
+      V y;
+      if constexpr (ORDER == 0)
+        y = x[u][j] * (inv * sc[u]); // cpp:324-325
+      else
+        y = (inv * x[u][j]) * sc[u]; // main.py:13-16
+      if ((NP < 0 || pend.store) && in_cols[u] && r0 + j < nrows)
+        st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W), y);
+      const T h = in_cols[u] ? hsum<T, W>(y) : (T)0;
+      acc[j] = u == 0 ? h : acc[j] + h;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U && !UM; u++) {
     if (!in[u])
       continue;
     if constexpr (NP > 0) {
@@ -1050,14 +1219,30 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     v[r] = v[r] * (s_cur[r] / m);
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  // the wave sums stay in lanes 62 / 63 (no broadcast), which write them:
+  // rows in pairs through one tree (wave_sum_pair), an odd last row alone
 #pragma unroll
-  for (int j = 0; j < R; j++) {
-    const T t = wave_sum(acc[j]);
-    if constexpr (PW) {
-      if (lane == 0 && r0 + j < nrows)
-        part[((size_t)(r0 + j) * ppr + p) * NW + wave] = t;
-    } else if (lane == 0) {
-      red[wave][j] = t;
+  for (int j = 0; j + 1 < R; j += 2) {
+    const T t = wave_sum_pair(acc[j], acc[j + 1]);
+    if (lane >= 62) {
+      const uint32_t jj = j + (lane - 62);
+      if constexpr (PW) {
+        if (r0 + jj < nrows)
+          part[((size_t)(r0 + jj) * ppr + p) * NW + wave] = t;
+      } else {
+        red[wave][jj] = t;
+      }
+    }
+  }
+  if constexpr (R % 2 == 1) {
+    const T t = wave_sum_l63(acc[R - 1]);
+    if (lane == 63) {
+      if constexpr (PW) {
+        if (r0 + R - 1 < nrows)
+          part[((size_t)(r0 + R - 1) * ppr + p) * NW + wave] = t;
+      } else {
+        red[wave][R - 1] = t;
+      }
     }
   }
   if constexpr (!PW) {

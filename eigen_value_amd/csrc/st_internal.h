@@ -77,8 +77,8 @@ bool round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem);
 // rounds, bit-identical results; FlatPending in st_device.h): npend pending
 // rounds' s and 1/s (oldest first), inv_cur = 1/s_cur, inv_next <- 1/s_{k+1};
 // flush = store the matrix only (after the loop; no row sums, no v)
-// rounds per store for a block: 4 on non-temporal blocks (>= 2 GiB), else 3
-// in fp64 and 4 in fp32 (profiles/r01_sweep_defer_rs.log)
+// rounds per store for a block: 4 (launch_flat_deferred's shapes,
+// profiles/r02_flat_map_shape_*.log)
 uint32_t defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem);
 constexpr uint32_t kDeferRoundsMax = 4;
 template <typename T>

@@ -605,7 +605,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         uint32_t ncols, uint32_t row0, T eps, uint32_t k,
                         uint32_t max_itr, uint32_t semantics, st_state* st,
                         const T* const* pend_s, const T* const* pend_inv,
-                        bool store, bool flush, hipStream_t stream)
+                        bool store, bool flush, uint32_t pt, hipStream_t stream)
 {
   constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
@@ -618,6 +618,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
   pd.inv_cur = inv_cur;
   pd.store = store ? 1u : 0u;
+  pd.pt = pt;
   const FlatGrid fg = flat_grid(grid);
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
                                   kBlock, 0, dev::kGatePlain, NP, U>),
@@ -630,10 +631,18 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                        0u, 0u, 0u, inv_next);
 }
 
-// rows per workgroup of the deferred rounds (profiles/r01_sweep_defer_rs.log):
-// non-temporal blocks take 2 rows in the read-only rounds and 4 in the
-// storing round (whose pending scales are then loaded once for 4 rows);
-// cached blocks 2 (fp64) or 4 (fp32) throughout
+// Launch shape of the deferred rounds by pending count NP
+// (tools/flat_map_sweep, profiles/r02_flat_map_shape_*.log: 32768^2,
+// 32768 / 16384 / 8192 x 65536 fp64 non-temporal, 8192^2 / 12288^2 /
+// 2880 x 23040 fp64 cached, 32768^2 and 8192^2 fp32):
+//   NP = 0            2 rows per workgroup; non-temporal blocks in the
+//                     piece-tiled order of 8 row groups (5-6 % at 32768^2)
+//   NP = 1, 2         4 rows (the pending rounds' column scales then serve
+//                     4 rows: 10-23 % at NP = 2), piece-tiled by 32 row
+//                     groups on non-temporal blocks, 16 on cached ones
+//   storing rounds    4 rows, row-major (10-12 %)
+// (the every-round flat round keeps 2 rows, row-major: the tiled order
+// and 4 rows lose 2-4 % there)
 template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
@@ -644,25 +653,26 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
-  constexpr int RR = (sizeof(T) == 4 && !NT) ? 4 : 2; // read-only rounds
-  constexpr int RS = NT ? 4 : RR;                      // storing rounds
-#define ST_NP(NPV, RV)                                                         \
+#define ST_NP(NPV, RV, PTV)                                                    \
   launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV>(                           \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
-    max_itr, semantics, st, pend_s, pend_inv, store, flush, stream)
-#define ST_NP_R(RV)                                                            \
-  switch (npend) {                                                             \
-  case 0: ST_NP(0, RV); break;                                                 \
-  case 1: ST_NP(1, RV); break;                                                 \
-  case 2: ST_NP(2, RV); break;                                                 \
-  default: ST_NP(3, RV); break;                                                \
-  }
+    max_itr, semantics, st, pend_s, pend_inv, store, flush, PTV, stream)
+  constexpr uint32_t kTile0 = NT ? 8u : 0u, kTile12 = NT ? 32u : 16u;
   if (store) {
-    ST_NP_R(RS)
+    switch (npend) {
+    case 0: ST_NP(0, 4, 0u); break;
+    case 1: ST_NP(1, 4, 0u); break;
+    case 2: ST_NP(2, 4, 0u); break;
+    default: ST_NP(3, 4, 0u); break;
+    }
   } else {
-    ST_NP_R(RR)
+    switch (npend) {
+    case 0: ST_NP(0, 2, kTile0); break;
+    case 1: ST_NP(1, 4, kTile12); break;
+    case 2: ST_NP(2, 4, kTile12); break;
+    default: ST_NP(3, 4, kTile12); break;
+    }
   }
-#undef ST_NP_R
 #undef ST_NP
 }
 
@@ -714,7 +724,14 @@ launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 uint32_t
 defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  return flat_round_nt(nrows, ncols, elem) ? 4u : (elem == 8 ? 3u : 4u);
+  // 4 everywhere: with the shapes above the read-only rounds with 1 or 2
+  // pending scalings cost about what the first one does, so a longer group
+  // pays on cached fp64 blocks too (8192^2: 0.0985 ms per round at m = 4 vs
+  // 0.1055 at m = 3, profiles/r02_flat_map_shape_f64_cached.log)
+  (void)nrows;
+  (void)ncols;
+  (void)elem;
+  return 4u;
 }
 
 template <typename T>

@@ -976,6 +976,20 @@ def test_cpp_kernel_tests():
     assert "similarity transform worked" in out.stdout
 
 
+def test_wave_reductions_bitwise():
+    """tests/cpp/test_reduce.hip: every wave-reduction form of st_device.h
+    (broadcast tree, lane-63 tree, the two-row tree of k_flat, stepwise
+    rows) gives the same bits on 4096 waves of mixed-magnitude data."""
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run(["make", "-s", "-C", os.path.join(here, "cpp"), "test_reduce"], check=True)
+    out = subprocess.run([os.path.join(here, "cpp", "test_reduce")], capture_output=True,
+                         text=True, timeout=120)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "wave reductions bit-identical" in out.stdout
+
+
 # ---------------------------------------------------------------------------
 # the whole solve in one workgroup (k_solve_small, n <= 128 fp64 / 256 fp32)
 # against the per-round launch loop: bit-identical λ, v, iteration count and
@@ -1035,7 +1049,7 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 
 
 # ---------------------------------------------------------------------------
-# deferred writes (blocks >= 144 MiB: the flat round stores A every 3rd/4th round
+# deferred writes (blocks >= 144 MiB: the flat round stores A every 4th round
 # and re-applies the pending scalings) against storing every round:
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------

@@ -31,8 +31,8 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 
 def rounds_per_store(n, elem, f64):
-    # st_defer_rounds: 4 on blocks of >= 2 GiB, else 3 fp64 / 4 fp32
-    return 4 if n * n * elem >= 2 << 30 else (3 if f64 else 4)
+    # st_defer_rounds: 4 on every block (round 2; round 1 took 3 on cached fp64)
+    return 4
 
 
 def run(args):

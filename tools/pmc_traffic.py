@@ -34,10 +34,10 @@ def flat_np(name):
 
 def flat_stores(name, m):
     """Whether a deferred k_flat instance stores the matrix: the launch with
-    m - 1 pending rounds, and on non-temporal blocks every 4-row instance
-    (the launchers' storing shape, which the final flush also takes)."""
-    args = [x.strip() for x in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
-    return flat_np(name) == m - 1 or (args[3] == "true" and args[4] == "4")
+    m - 1 pending rounds.  (A final flush after a partial group also stores,
+    with fewer pending rounds and the same instance as a read-only round;
+    the profiled runs end on whole store cycles, so they have none.)"""
+    return flat_np(name) == m - 1
 
 
 def short(name, m=3):
@@ -78,7 +78,7 @@ def main():
     nb = 1.0 * a.n * a.n * a.elem
     # deferred writes: m rounds per store (st_defer_rounds); a storing
     # launch moves 2 N^2 b, the others read N^2 b
-    m = 4 if nb >= 2 ** 31 else (3 if a.elem == 8 else 4)
+    m = 4  # st_defer_rounds (round 2: every block)
     fetch, write = load_pmc(a.fetch, m), load_pmc(a.write, m)
     trace = load_trace(a.trace, m) if a.trace else {}
     algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb}
