@@ -657,7 +657,14 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV>(                           \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, store, flush, PTV, stream)
-  constexpr uint32_t kTile0 = NT ? 8u : 0u, kTile12 = NT ? 32u : 16u;
+#ifndef ST_DEFER_R0_CACHED // shape probes (tools/defer_shape_probe.sh)
+#define ST_DEFER_R0_CACHED 2
+#endif
+#ifndef ST_DEFER_PT0_CACHED
+#define ST_DEFER_PT0_CACHED 0u
+#endif
+  constexpr int kR0 = NT ? 2 : ST_DEFER_R0_CACHED;
+  constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED, kTile12 = NT ? 32u : 16u;
   if (store) {
     switch (npend) {
     case 0: ST_NP(0, 4, 0u); break;
@@ -667,7 +674,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
     }
   } else {
     switch (npend) {
-    case 0: ST_NP(0, 2, kTile0); break;
+    case 0: ST_NP(0, kR0, kTile0); break;
     case 1: ST_NP(1, 4, kTile12); break;
     case 2: ST_NP(2, 4, kTile12); break;
     default: ST_NP(3, 4, kTile12); break;

@@ -65,6 +65,13 @@ for s in $STEPS; do
         step "defer_${K}${N}_${DT}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --events "$D/events.json"
         python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --trace "$D/prof/run_kernel_trace.csv" --events "$D/events.json" --json "$D/cycle.json" | tee -a "$OUT/session.log"
       done ;;
+    defer_pmc) # HBM bytes per deferred launch (separate FETCH / WRITE passes)
+      for W in "random 32768 f64" "random 32768 f32"; do
+        set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_pmc_${K}${N}_${DT}"; mkdir -p "$D"
+        step "defer_fetch_${K}${N}_${DT}" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/fetch" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --cycles 3
+        step "defer_write_${K}${N}_${DT}" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/write" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --cycles 3
+        python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --fetch "$D/fetch/run_counter_collection.csv" --write "$D/write/run_counter_collection.csv" --json "$D/pmc.json" | tee -a "$OUT/session.log"
+      done ;;
     profile_f32) # configs[4]: 32768^2 fp32 every-round flat round, trace + PMC passes
       D="$OUT/random32768_f32"
       step prof_f32 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind random --n 32768 --dtype f32 --steps 50 --warmup 3 --no-cpu --no-north-star --no-headline
