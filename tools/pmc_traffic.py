@@ -37,7 +37,10 @@ def flat_stores(name, m):
     m - 1 pending rounds.  (A final flush after a partial group also stores,
     with fewer pending rounds and the same instance as a read-only round;
     the profiled runs end on whole store cycles, so they have none.)"""
-    return flat_np(name) == m - 1
+    args = [x.strip() for x in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
+    # a 4-row launch with no pending round only ever stores (the flush after
+    # a partial group; the read-only NP = 0 rounds take 2 rows)
+    return flat_np(name) == m - 1 or (flat_np(name) == 0 and args[4] == "4")
 
 
 def short(name, m=3):
