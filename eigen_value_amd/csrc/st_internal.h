@@ -77,10 +77,10 @@ bool round_flat_pays(uint32_t nrows, uint32_t ncols, size_t elem);
 // rounds, bit-identical results; FlatPending in st_device.h): npend pending
 // rounds' s and 1/s (oldest first), inv_cur = 1/s_cur, inv_next <- 1/s_{k+1};
 // flush = store the matrix only (after the loop; no row sums, no v)
-// rounds per store for a block: 4 (launch_flat_deferred's shapes,
-// profiles/r02_flat_map_shape_*.log)
+// rounds per store for a block: 6 (launch_flat_deferred's shapes,
+// profiles/r02_flat_map_np5_*.log)
 uint32_t defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem);
-constexpr uint32_t kDeferRoundsMax = 4;
+constexpr uint32_t kDeferRoundsMax = 6;
 template <typename T>
 int launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur,
                                T* s_next, T* inv_next, T* part, T* v,

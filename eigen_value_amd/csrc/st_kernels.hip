@@ -632,15 +632,18 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 }
 
 // Launch shape of the deferred rounds by pending count NP
-// (tools/flat_map_sweep, profiles/r02_flat_map_shape_*.log: 32768^2,
-// 32768 / 16384 / 8192 x 65536 fp64 non-temporal, 8192^2 / 12288^2 /
-// 2880 x 23040 fp64 cached, 32768^2 and 8192^2 fp32):
+// (tools/flat_map_sweep, profiles/r02_flat_map_shape_*.log and
+// r02_flat_map_np5_*.log: 32768^2, 32768 / 16384 / 8192 x 65536 fp64
+// non-temporal, 8192^2 / 12288^2 / 2880 x 23040 fp64 cached, 32768^2 and
+// 8192^2 fp32):
 //   NP = 0            2 rows per workgroup; non-temporal blocks in the
 //                     piece-tiled order of 8 row groups (5-6 % at 32768^2)
 //   NP = 1, 2         4 rows (the pending rounds' column scales then serve
 //                     4 rows: 10-23 % at NP = 2), piece-tiled by 32 row
 //                     groups on non-temporal blocks, 16 on cached ones
-//   storing rounds    4 rows, row-major (10-12 %)
+//   NP = 3, 4         4 rows; row-major on non-temporal blocks, tiled by 32
+//                     on cached ones
+//   storing rounds    4 rows, row-major (10-16 %)
 // (the every-round flat round keeps 2 rows, row-major: the tiled order
 // and 4 rows lose 2-4 % there)
 template <typename T, int W, int ORDER, bool NT>
@@ -664,20 +667,25 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 #define ST_DEFER_PT0_CACHED 0u
 #endif
   constexpr int kR0 = NT ? 2 : ST_DEFER_R0_CACHED;
-  constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED, kTile12 = NT ? 32u : 16u;
+  constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED;
+  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = NT ? 0u : 32u;
+  static_assert(kDeferRoundsMax == 6, "one case per pending count below");
   if (store) {
     switch (npend) {
     case 0: ST_NP(0, 4, 0u); break;
     case 1: ST_NP(1, 4, 0u); break;
     case 2: ST_NP(2, 4, 0u); break;
-    default: ST_NP(3, 4, 0u); break;
+    case 3: ST_NP(3, 4, 0u); break;
+    case 4: ST_NP(4, 4, 0u); break;
+    default: ST_NP(5, 4, 0u); break;
     }
   } else {
     switch (npend) {
     case 0: ST_NP(0, kR0, kTile0); break;
     case 1: ST_NP(1, 4, kTile12); break;
     case 2: ST_NP(2, 4, kTile12); break;
-    default: ST_NP(3, 4, kTile12); break;
+    case 3: ST_NP(3, 4, kTile34); break;
+    default: ST_NP(4, 4, kTile34); break;
     }
   }
 #undef ST_NP
@@ -731,14 +739,16 @@ launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 uint32_t
 defer_rounds(uint32_t nrows, uint32_t ncols, size_t elem)
 {
-  // 4 everywhere: with the shapes above the read-only rounds with 1 or 2
-  // pending scalings cost about what the first one does, so a longer group
-  // pays on cached fp64 blocks too (8192^2: 0.0985 ms per round at m = 4 vs
-  // 0.1055 at m = 3, profiles/r02_flat_map_shape_f64_cached.log)
+  // 6 everywhere: with the shapes above a read-only round with 1 ... 4
+  // pending scalings costs 0-10 % more than the first one, so the group
+  // that spreads one store over 6 rounds is 3-5 % faster per round than 4
+  // (32768^2 fp64 1.55 vs 1.62 ms, 8192 x 65536 0.818 vs 0.842, 32768^2
+  // fp32 0.762 vs 0.798; profiles/r02_flat_map_np5_*.log), and even on
+  // cached fp64 blocks, where round 1 took 3
   (void)nrows;
   (void)ncols;
   (void)elem;
-  return 4u;
+  return kDeferRoundsMax;
 }
 
 template <typename T>

@@ -331,7 +331,7 @@ class DeviceSolver:
         Matrices of n <= 128 (fp64) / 256 (fp32) run the whole solve in one
         workgroup launch (bit-identical); ``round_loop`` forces one launch per
         round instead (``ST_FLAG_ROUND_LOOP``).  Matrices of >= 144 MiB
-        store the transformed matrix every 4th round
+        store the transformed matrix every 6th round
         (``defer_rounds``) and re-apply the pending scalings in registers
         (identical results and final matrix, a third to 3/8 fewer bytes);
         ``write_every_round`` stores it every round

@@ -81,7 +81,7 @@ class EigenValue:
         ``round_loop`` keeps one launch per round where the whole solve would
         fit one workgroup (``ST_FLAG_ROUND_LOOP``; identical results);
         ``write_every_round`` stores the matrix every round where the flat
-        round would store it every 4th (``ST_FLAG_WRITE_EVERY_ROUND``;
+        round would store it every 6th (``ST_FLAG_WRITE_EVERY_ROUND``;
         identical results).
 
         Returns ``(λ, v, ts_ms, iterations, stats_dict)``."""

@@ -92,7 +92,7 @@ typedef struct st_options
                                 /* transform (input never written)         */
 #define ST_FLAG_WRITE_EVERY_ROUND 8u /* store the matrix every round; by    */
                                 /* default the flat round (>= 144 MiB)      */
-                                /* stores it every 4th round (st_defer_     */
+                                /* stores it every 6th round (st_defer_     */
                                 /* rounds) and re-applies                   */
                                 /* the pending scalings in registers:       */
                                 /* identical results, fewer bytes           */
@@ -369,7 +369,7 @@ int st_recip_f32(const float* d_s, float* d_inv, unsigned int n, void* stream);
 int st_recip_f64(const double* d_s, double* d_inv, unsigned int n,
                  void* stream);
 /* rounds per store of the deferred flat round on a block (dtype 0 = f32,
- * 1 = f64): 4 on every block (the arguments are kept for future shapes) */
+ * 1 = f64): 6 on every block (the arguments are kept for future shapes) */
 unsigned int st_defer_rounds(unsigned int nrows, unsigned int ncols,
                              int dtype);
 

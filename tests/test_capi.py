@@ -127,12 +127,12 @@ def test_sharded_partition_rejects_empty_rank():
 def test_launch_policy_queries():
     """Host-side policy exported by the library (no device needed): the flat
     round from 144 MiB and the deferred-write depth
-    (4 rounds per store on every block since round 2's launch shapes)."""
+    (6 rounds per store on every block since round 2's launch shapes)."""
     L = _lib.load()
     assert L.st_round_flat_pays(6144, 6144, 0) == 1        # 144 MiB fp32
     assert L.st_round_flat_pays(4096, 4096, 1) == 0        # 128 MiB fp64
     assert L.st_round_flat_pays(8192, 8192, 1) == 1
-    assert L.st_defer_rounds(8192, 8192, 1) == 4
-    assert L.st_defer_rounds(8192, 8192, 0) == 4
-    assert L.st_defer_rounds(32768, 32768, 1) == 4
-    assert L.st_defer_rounds(16384, 16384, 1) == 4         # 2 GiB: non-temporal
+    assert L.st_defer_rounds(8192, 8192, 1) == 6
+    assert L.st_defer_rounds(8192, 8192, 0) == 6
+    assert L.st_defer_rounds(32768, 32768, 1) == 6
+    assert L.st_defer_rounds(16384, 16384, 1) == 6         # 2 GiB: non-temporal

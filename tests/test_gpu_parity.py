@@ -1049,7 +1049,7 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 
 
 # ---------------------------------------------------------------------------
-# deferred writes (blocks >= 144 MiB: the flat round stores A every 4th round
+# deferred writes (blocks >= 144 MiB: the flat round stores A every 6th round
 # and re-applies the pending scalings) against storing every round:
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------
@@ -1062,10 +1062,11 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 def test_deferred_writes_bitwise(solver, dt, n, sem):
     assert dev.flat_round_pays(n, n, TD[dt])
     base = dev.generate("random", n, TD[dt], seed=4, device=DEV)
-    # fixed round counts ending at every residue mod 3 and mod 4 (the final
-    # flush), a converging solve, and max_itr = 1
+    # fixed round counts ending at every residue mod 6 (the final flush), a
+    # converging solve, and max_itr = 1
     for kw in (dict(eps=0.0, max_itr=7), dict(eps=0.0, max_itr=8), dict(eps=0.0, max_itr=9),
-               dict(eps=0.0, max_itr=10), dict(), dict(eps=1e-9), dict(max_itr=1)):
+               dict(eps=0.0, max_itr=10), dict(eps=0.0, max_itr=11), dict(eps=0.0, max_itr=12),
+               dict(), dict(eps=1e-9), dict(max_itr=1)):
         a1, a2 = base.clone(), base.clone()
         r1 = solver.solve(a1, inplace=True, semantics=sem, **kw)
         r2 = solver.solve(a2, inplace=True, semantics=sem, write_every_round=True, **kw)

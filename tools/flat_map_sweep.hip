@@ -44,7 +44,10 @@ using namespace st::dev;
 
 constexpr int kSeq = 8;
 constexpr int kReps = 7;
-constexpr int kRing = 5; // s_k and up to 3 pending + 1
+constexpr int kRing = 7; // s_k and up to 5 pending + 1
+static std::vector<unsigned> g_pts = { 0, 16 };
+static int g_store_np = 3; // FMS_STORE_NP: the pending count of the storing round
+static int g_max_np = 3;   // FMS_MAX_NP (<= 5)
 
 template <typename F>
 static float
@@ -93,7 +96,7 @@ one(const Block<T>& b, unsigned pt)
   const unsigned ppr = (b.n + 256 * W * U - 1) / (256 * W * U);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   constexpr int NPK = NP < 0 ? -1 : NP;
-  const bool store = NP < 0 || NP == 3;
+  const bool store = NP < 0 || NP == g_store_np;
   float ms = time_seq([&](int k) {
     FlatPending<T, NPK> pd{};
     for (int i = 0; i < (NP > 0 ? NP : 0); i++) {
@@ -113,7 +116,6 @@ one(const Block<T>& b, unsigned pt)
   std::fflush(stdout);
 }
 
-static std::vector<unsigned> g_pts = { 0, 16 };
 
 template <typename T, bool NT, int R, int NP>
 static void
@@ -133,6 +135,10 @@ by_np(const Block<T>& b)
   by_pt<T, NT, R, 1>(b);
   by_pt<T, NT, R, 2>(b);
   by_pt<T, NT, R, 3>(b);
+  if (g_max_np >= 4)
+    by_pt<T, NT, R, 4>(b);
+  if (g_max_np >= 5)
+    by_pt<T, NT, R, 5>(b);
 }
 
 template <typename T, bool NT>
@@ -207,6 +213,10 @@ main(int argc, char** argv)
     return 1;
   }
   const bool f64 = std::strcmp(argv[1], "f64") == 0;
+  if (const char* e = std::getenv("FMS_STORE_NP"))
+    g_store_np = std::atoi(e);
+  if (const char* e = std::getenv("FMS_MAX_NP"))
+    g_max_np = std::atoi(e);
   if (const char* e = std::getenv("FMS_PT")) { // e.g. FMS_PT=0,4,8,16,32
     g_pts.clear();
     for (const char* q = e; *q;) {

@@ -81,7 +81,7 @@ def main():
     nb = 1.0 * a.n * a.n * a.elem
     # deferred writes: m rounds per store (st_defer_rounds); a storing
     # launch moves 2 N^2 b, the others read N^2 b
-    m = 4  # st_defer_rounds (round 2: every block)
+    m = 6  # st_defer_rounds (round 2: every block)
     fetch, write = load_pmc(a.fetch, m), load_pmc(a.write, m)
     trace = load_trace(a.trace, m) if a.trace else {}
     algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb}
