@@ -1028,11 +1028,12 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       const uint32_t q = bb - (rg - 1) * pr;
       p = q < pa ? q : q + nfull;
     }
-  } else if (NP >= 0 && pend.pt != 0) {
-    // piece-tiled order (deferred rounds): pt row groups of one piece run
-    // back to back (the XCDs take every 8th), so the workgroups a CU runs
-    // in turn share the piece's column scales - s_k and the pending
-    // rounds' - in its L1 instead of refetching them from L2
+  } else if (SPLIT == 0 && pend.pt != 0) {
+    // piece-tiled order: pt row groups of one piece run back to back (the
+    // XCDs take every 8th), so the workgroups a CU runs in turn share the
+    // piece's column scales - s_k and the pending rounds' - in its L1
+    // instead of refetching them from L2 (deferred rounds; and the
+    // every-round launch on non-temporal blocks, tiles of 4)
     const uint32_t pt = pend.pt, ng = (nrows + R - 1) / R;
     const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
     const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;

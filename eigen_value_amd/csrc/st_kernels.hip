@@ -517,6 +517,13 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
   const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   const FlatGrid fg = flat_grid(grid);
+  // non-temporal blocks walk the pieces in tiles of 4 row groups
+  // (FlatPending::pt; tools/flat_map_sweep FMS_EVERY=1,
+  // profiles/r02_flat_map_every_*.log: 32768^2 fp64 2.625 vs 2.688 ms, fp32
+  // 1.301 vs 1.336, 16384 / 8192 x 65536 -1.8 / -1.0 %); cached blocks keep
+  // the row-major order (8192^2 fp64: tiles 0.7 % slower)
+  dev::FlatPending<T, -1> pe{};
+  pe.pt = NT ? 4u : 0u;
   if constexpr (kFlatFusedStats) {
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
@@ -525,7 +532,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                    dev::kGatePlain, -1, U>),
       fg.grid,
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
-      st, eps, max_itr, semantics, 0u, 0u, 0u, dev::FlatPending<T, -1>{}, fg.gx2);
+      st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, s_cur, v, row0);
   } else {
@@ -537,8 +544,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
       (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt, kBlock, 0,
                    dev::kGatePlain, -1, U>),
       fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
-      row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u,
-      dev::FlatPending<T, -1>{}, fg.gx2);
+      row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, nullptr, nullptr, 0u);
   }
@@ -639,11 +645,17 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 //   NP = 0            2 rows per workgroup; non-temporal blocks in the
 //                     piece-tiled order of 8 row groups (5-6 % at 32768^2)
 //   NP = 1, 2         4 rows (the pending rounds' column scales then serve
-//                     4 rows: 10-23 % at NP = 2), piece-tiled by 32 row
-//                     groups on non-temporal blocks, 16 on cached ones
-//   NP = 3, 4         4 rows; row-major on non-temporal blocks, tiled by 32
-//                     on cached ones
-//   storing rounds    4 rows, row-major (10-16 %)
+//                     4 rows: 10-23 % at NP = 2; NP = 2 on non-temporal
+//                     blocks 8 rows, 1-2 %), piece-tiled by 32 row groups
+//                     on non-temporal blocks, 16 on cached ones
+//   NP = 3, 4         8 rows (the column scales of 3 - 4 pending rounds then
+//                     serve 8 rows: 3-10 % over 4 rows, NP = 4 at 32768^2
+//                     fp64 1.230 vs 1.351 ms); row-major on non-temporal
+//                     blocks, tiled by 16 on cached ones
+//                     (profiles/r02_flat_map_r8_*.log)
+//   storing rounds    row-major; 4 rows (10-16 % over 2), 8 on non-temporal
+//                     blocks when rounds are pending (3 %: 32768^2 fp64
+//                     2.852 vs 2.931 ms, 8192 x 65536 1.434 vs 1.481)
 // (the every-round flat round keeps 2 rows, row-major: the tiled order
 // and 4 rows lose 2-4 % there)
 template <typename T, int W, int ORDER, bool NT>
@@ -668,24 +680,28 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 #endif
   constexpr int kR0 = NT ? 2 : ST_DEFER_R0_CACHED;
   constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED;
-  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = NT ? 0u : 32u;
+  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = NT ? 0u : 16u;
+  // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
+  // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
+  constexpr int kRS = NT ? 8 : 4;
+  constexpr int kR2 = NT ? 8 : 4; // NP = 2: 1-2 % with 8 rows, non-temporal only
   static_assert(kDeferRoundsMax == 6, "one case per pending count below");
   if (store) {
     switch (npend) {
     case 0: ST_NP(0, 4, 0u); break;
-    case 1: ST_NP(1, 4, 0u); break;
-    case 2: ST_NP(2, 4, 0u); break;
-    case 3: ST_NP(3, 4, 0u); break;
-    case 4: ST_NP(4, 4, 0u); break;
-    default: ST_NP(5, 4, 0u); break;
+    case 1: ST_NP(1, kRS, 0u); break;
+    case 2: ST_NP(2, kRS, 0u); break;
+    case 3: ST_NP(3, kRS, 0u); break;
+    case 4: ST_NP(4, kRS, 0u); break;
+    default: ST_NP(5, kRS, 0u); break;
     }
   } else {
     switch (npend) {
     case 0: ST_NP(0, kR0, kTile0); break;
     case 1: ST_NP(1, 4, kTile12); break;
-    case 2: ST_NP(2, 4, kTile12); break;
-    case 3: ST_NP(3, 4, kTile34); break;
-    default: ST_NP(4, 4, kTile34); break;
+    case 2: ST_NP(2, kR2, kTile12); break;
+    case 3: ST_NP(3, 8, kTile34); break;
+    default: ST_NP(4, 8, kTile34); break;
     }
   }
 #undef ST_NP

@@ -13,7 +13,7 @@
 //               over the XCDs (FlatPending::pt; FMS_PT=0,4,8,... picks the
 //               values, default 0,16; g = 16 ... 1024 in
 //               profiles/r02_flat_map_tiles_*.log)
-// and R = 2, 4 rows per workgroup, NP = -1 (every-round store), 0, 1, 2 and
+// and R = 2, 4 rows per workgroup (4, 8 with FMS_R8=1), NP = -1 (every-round store), 0, 1, 2 and
 // 3 (+ store, the storing round of a 4-round group).  Median of 7
 // sequences of 8 launches (k = 0..7, so the ALT reversal alternates).
 //
@@ -48,6 +48,9 @@ constexpr int kRing = 7; // s_k and up to 5 pending + 1
 static std::vector<unsigned> g_pts = { 0, 16 };
 static int g_store_np = 3; // FMS_STORE_NP: the pending count of the storing round
 static int g_max_np = 3;   // FMS_MAX_NP (<= 5)
+static bool g_r8 = false;  // FMS_R8=1: 8 rows per workgroup instead of 2 and 4
+static bool g_every = false; // FMS_EVERY=1: the every-round launch (NP = -1) only,
+                             // R = 1, 2, 4 by PT
 
 template <typename F>
 static float
@@ -122,7 +125,7 @@ static void
 by_pt(const Block<T>& b)
 {
   for (unsigned pt : g_pts)
-    if (NP >= 0 || pt == 0)
+    if (NP >= 0 || pt == 0 || g_every)
       one<T, NT, R, NP>(b, pt);
 }
 
@@ -188,6 +191,24 @@ run(unsigned nr, unsigned n)
       by_np_quick<T, true>(b);
     else
       by_np_quick<T, false>(b);
+  } else if (g_every) {
+    if (nt) {
+      by_pt<T, true, 1, -1>(b);
+      by_pt<T, true, 2, -1>(b);
+      by_pt<T, true, 4, -1>(b);
+    } else {
+      by_pt<T, false, 1, -1>(b);
+      by_pt<T, false, 2, -1>(b);
+      by_pt<T, false, 4, -1>(b);
+    }
+  } else if (g_r8) {
+    if (nt) {
+      by_np<T, true, 4>(b);
+      by_np<T, true, 8>(b);
+    } else {
+      by_np<T, false, 4>(b);
+      by_np<T, false, 8>(b);
+    }
   } else if (nt) {
     by_np<T, true, 2>(b);
     by_np<T, true, 4>(b);
@@ -217,6 +238,8 @@ main(int argc, char** argv)
     g_store_np = std::atoi(e);
   if (const char* e = std::getenv("FMS_MAX_NP"))
     g_max_np = std::atoi(e);
+  g_r8 = std::getenv("FMS_R8") != nullptr;
+  g_every = std::getenv("FMS_EVERY") != nullptr;
   if (const char* e = std::getenv("FMS_PT")) { // e.g. FMS_PT=0,4,8,16,32
     g_pts.clear();
     for (const char* q = e; *q;) {

@@ -15,8 +15,10 @@ for 16 B/lane streaming stores.  Launches that did no work (device-gated
 rounds after convergence) are dropped (< 10 % of the median traffic).
 The kernel trace gives the per-launch duration of the same command.
 Deferred-write launches of k_flat (template argument NP >= 0) are reported
-as k_flat_np<NP> against their own algorithmic bytes (N^2 b read-only,
-2 N^2 b for the storing launch); k_flat is the every-round transform.
+as k_flat_np<NP> against their own algorithmic bytes (N^2 b read-only), or
+k_flat_np<NP>_store (2 N^2 b) for the launches whose WRITE_SIZE shows they
+stored the block (one instance serves both); k_flat is the every-round
+transform.  Launches are matched across the three runs by dispatch order.
 """
 import argparse
 import collections
@@ -32,38 +34,23 @@ def flat_np(name):
     return int(args[11]) if len(args) > 11 else -1
 
 
-def flat_stores(name, m):
-    """Whether a deferred k_flat instance stores the matrix: the launch with
-    m - 1 pending rounds.  (A final flush after a partial group also stores,
-    with fewer pending rounds and the same instance as a read-only round;
-    the profiled runs end on whole store cycles, so they have none.)"""
-    args = [x.strip() for x in name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")]
-    # a 4-row launch with no pending round only ever stores (the flush after
-    # a partial group; the read-only NP = 0 rounds take 2 rows)
-    return flat_np(name) == m - 1 or (flat_np(name) == 0 and args[4] == "4")
-
-
-def short(name, m=3):
+def short(name):
     base = name.split("(")[0].replace("void ", "")
     k = base.split("<")[0].split("::")[-1]
     if k == "k_flat" and flat_np(name) >= 0:   # deferred writes (st_device.h FlatPending)
-        k = f"k_flat_np{flat_np(name)}" + ("_store" if flat_stores(name, m) else "")
+        k = f"k_flat_np{flat_np(name)}"
     return k
 
 
-def load_pmc(path, m):
+def load_seq(path, value):
+    """Per kernel instance, its launches in dispatch order."""
     out = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        out[(short(r["Kernel_Name"], m), r["Kernel_Name"].split("(")[0])].append(
-            float(r["Counter_Value"]))
-    return out
-
-
-def load_trace(path, m):
-    out = collections.defaultdict(list)
-    for r in csv.DictReader(open(path)):
-        dur = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # ms
-        out[(short(r["Kernel_Name"], m), r["Kernel_Name"].split("(")[0])].append(dur)
+    rows = list(csv.DictReader(open(path)))
+    key = "Dispatch_Id" if rows and "Dispatch_Id" in rows[0] else None
+    if key:
+        rows.sort(key=lambda r: int(r[key]))
+    for r in rows:
+        out[r["Kernel_Name"].split("(")[0]].append(value(r))
     return out
 
 
@@ -82,32 +69,59 @@ def main():
     # deferred writes: m rounds per store (st_defer_rounds); a storing
     # launch moves 2 N^2 b, the others read N^2 b
     m = 6  # st_defer_rounds (round 2: every block)
-    fetch, write = load_pmc(a.fetch, m), load_pmc(a.write, m)
-    trace = load_trace(a.trace, m) if a.trace else {}
+    fetch = load_seq(a.fetch, lambda r: float(r["Counter_Value"]))
+    write = load_seq(a.write, lambda r: float(r["Counter_Value"]))
+    trace = load_seq(a.trace, lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                     * 1e-6) if a.trace else {}
     algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb}
     for npend in range(m):
         algo[f"k_flat_np{npend}"] = nb
         algo[f"k_flat_np{npend}_store"] = 2.0 * nb
-    entries = []
-    for key in sorted(fetch):
-        kname, full = key
-        if kname not in algo or f"<{a.dtype}," not in full:
+    # one deferred instance serves a read-only round and a storing one
+    # (the storing round of a group, a final flush): the i-th launch of an
+    # instance is the same launch in the three runs of the command, and it
+    # stored the matrix if its WRITE_SIZE is at least half the block
+    groups = collections.defaultdict(lambda: ([], [], []))
+    for full, f in fetch.items():
+        kname = short(full)
+        if f"<{a.dtype}," not in full or (kname not in algo):
             continue
-        f = fetch[key]
-        w = write.get(key, [])
+        w = write.get(full, [])
+        d = trace.get(full, [])
+        if len(d) != len(f):
+            # a trace of another command length: its launches stored where
+            # they took well over the instance's median (a storing round
+            # moves twice the bytes)
+            med_d = statistics.median(d) if d else 0.0
+            d_ro = [x for x in d if x <= 1.5 * med_d]
+            d_st = [x for x in d if x > 1.5 * med_d]
+            d = None
+        for i, fv in enumerate(f):
+            wv = w[i] if i < len(w) else 0.0
+            label = kname
+            if kname.startswith("k_flat_np") and wv * 1024.0 >= 0.5 * nb:
+                label += "_store"
+            g = groups[(label, full)]
+            g[0].append(fv)
+            g[1].append(wv)
+            if d is not None:
+                g[2].append(d[i])
+            elif not g[2]:
+                g[2].extend(d_st if label.endswith("_store") and kname != "k_flat" else d_ro)
+    entries = []
+    for (kname, full), (f, w, d) in sorted(groups.items()):
         med = statistics.median(f)
         keep = [i for i, x in enumerate(f) if x >= 0.1 * med]
         f_kb = statistics.median([f[i] for i in keep])
-        w_kb = statistics.median([w[i] for i in keep if i < len(w)]) if w else 0.0
+        w_kb = statistics.median([w[i] for i in keep])
         hbm = (2.0 * f_kb + w_kb) * 1024.0
         e = {"kernel": kname, "instance": full, "launches": len(f), "launches_used": len(keep),
              "fetch_size_kib": f_kb, "write_size_kib": w_kb,
              "hbm_bytes_per_launch": hbm, "correction": "FETCH_SIZE x2 (gfx950 wide-stream read)",
              "algorithmic_bytes": algo[kname], "traffic_over_algorithmic": hbm / algo[kname]}
-        if key in trace:
-            d = trace[key]
-            dm = statistics.median(d)
-            dk = [x for x in d if x >= 0.1 * dm]
+        dk = [d[i] for i in keep if i < len(d)] if len(d) == len(f) else \
+            [x for x in d if x >= 0.1 * statistics.median(d)] if d else []
+        if dk:
             e["trace_ms_avg"] = sum(dk) / len(dk)
             e["trace_launches"] = len(d)
             e["achieved_gbs_from_trace"] = algo[kname] / (e["trace_ms_avg"] * 1e-3) / 1e9
