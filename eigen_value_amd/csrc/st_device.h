@@ -250,6 +250,9 @@ ld(const V* p)
 #ifndef ST_FLAT_UNMASKED
 #define ST_FLAT_UNMASKED 1
 #endif
+#ifndef ST_DEFER_STORE_NT
+#define ST_DEFER_STORE_NT 0
+#endif
 template <typename T>
 __device__ __forceinline__ T
 ld_row(const T* p)
@@ -1064,6 +1067,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // fp64; the every-round and NP = 0 forms lose up to 3 %,
   // profiles/r02_flat_map_ab_*.log)
   constexpr bool UM = SPLIT == 0 && NP > 0 && ST_FLAT_UNMASKED;
+  // the deferred rounds' stores (probe switch ST_DEFER_STORE_NT: non-temporal
+  // on cached blocks too)
+  constexpr bool NTS = NT || (NP >= 0 && ST_DEFER_STORE_NT);
   uint32_t cl[U]; // the column each lane loads
 #pragma unroll
   for (int u = 0; u < U; u++)
@@ -1172,7 +1178,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       else
         y = (inv * x[u][j]) * sc[u]; // main.py:13-16
       if ((NP < 0 || pend.store) && in_cols[u] && r0 + j < nrows)
-        st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W), y);
+        st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W), y);
       const T h = in_cols[u] ? hsum<T, W>(y) : (T)0;
       acc[j] = u == 0 ? h : acc[j] + h;
     }
@@ -1207,7 +1213,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         else
           y = (inv * x[u][j]) * sc[u]; // main.py:13-16
         if (NP < 0 || pend.store)
-          st<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
+          st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
                     y);
         acc[j] = u == 0 ? hsum<T, W>(y) : acc[j] + hsum<T, W>(y);
       }

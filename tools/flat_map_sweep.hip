@@ -90,12 +90,13 @@ struct Block
   st_state* st;
 };
 
-template <typename T, bool NT, int R, int NP>
+template <typename T, bool NT, int R, int NP, int UF = 0>
 static void
 one(const Block<T>& b, unsigned pt)
 {
   constexpr int W = 16 / sizeof(T);
-  constexpr int U = (sizeof(T) == 8 && !NT) ? 2 : 1; // kFlatU (vector path)
+  // kFlatU (vector path), or UF chunks per piece
+  constexpr int U = UF ? UF : (sizeof(T) == 8 && !NT) ? 2 : 1;
   const unsigned ppr = (b.n + 256 * W * U - 1) / (256 * W * U);
   const unsigned grid = (b.nr + R - 1) / R * ppr;
   constexpr int NPK = NP < 0 ? -1 : NP;
@@ -114,19 +115,19 @@ one(const Block<T>& b, unsigned pt)
                        ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
   });
   const double bytes = (store ? 2.0 : 1.0) * b.nr * (double)b.n * sizeof(T);
-  std::printf("  NP=%2d R=%d PT=%5u nt=%d  %8.4f ms  %7.1f GB/s\n", NP, R, pt, (int)NT, ms,
-              bytes / (ms * 1e-3) / 1e9);
+  std::printf("  NP=%2d R=%d PT=%5u nt=%d%s  %8.4f ms  %7.1f GB/s\n", NP, R, pt, (int)NT,
+              UF ? (UF == 2 ? " U=2" : " U=4") : "", ms, bytes / (ms * 1e-3) / 1e9);
   std::fflush(stdout);
 }
 
 
-template <typename T, bool NT, int R, int NP>
+template <typename T, bool NT, int R, int NP, int UF = 0>
 static void
 by_pt(const Block<T>& b)
 {
   for (unsigned pt : g_pts)
     if (NP >= 0 || pt == 0 || g_every)
-      one<T, NT, R, NP>(b, pt);
+      one<T, NT, R, NP, UF>(b, pt);
 }
 
 template <typename T, bool NT, int R>
@@ -192,7 +193,11 @@ run(unsigned nr, unsigned n)
     else
       by_np_quick<T, false>(b);
   } else if (g_every) {
-    if (nt) {
+    if (nt && std::getenv("FMS_U2")) { // 8 KB pieces on a non-temporal block
+      by_pt<T, true, 2, -1>(b);
+      by_pt<T, true, 2, -1, 2>(b);
+      by_pt<T, true, 1, -1, 2>(b);
+    } else if (nt) {
       by_pt<T, true, 1, -1>(b);
       by_pt<T, true, 2, -1>(b);
       by_pt<T, true, 4, -1>(b);
