@@ -182,6 +182,40 @@ template <typename T, int W, bool NT>
 constexpr int kFlatU =
   (W == 1 ? (int)(16 / sizeof(T)) : 1) * ((sizeof(T) == 8 && !NT) ? 2 : 1);
 
+// Shape of the every-round flat launch (tools/flat_map_sweep FMS_EVERY=1,
+// profiles/r02_flat_map_every_*.log, two repeats each):
+//   non-temporal blocks  2 rows per workgroup, pieces walked in tiles of 4
+//                        row groups (32768^2 fp64 2.625 vs 2.688 ms, fp32
+//                        1.301 vs 1.336, 16384 / 8192 x 65536 -1.8 / -1.0 %)
+//   cached fp64 blocks   1 row (8 KB pieces), tiles of 8 rows from 384 MiB
+//                        and of 4 below: 8192^2 0.1536 / 0.1528 vs 0.1545 /
+//                        0.1539 ms (2 rows, row-major), 12288^2 -0.5 %,
+//                        6144^2 -1 % (tiles of 4; 8 lose 2 % there); the
+//                        whole round on the weak-scaled rank blocks, k_parts
+//                        included (tools/split_cost.py,
+//                        profiles/r02_every_cached_ab_split_cost.log):
+//                        5824 x 11648 0.162 vs 0.171 ms, 4096 x 16384 0.156
+//                        vs 0.159, 2880 x 23040 0.155 vs 0.159
+//   cached fp32 blocks   2 rows, row-major (1 row or tiles lose 0-3 %)
+// Which rows a workgroup takes, and in what order, changes no result.
+#ifndef ST_EVERY_CACHED_R1 // A/B probe: 0 = round 2's 2 rows, row-major
+#define ST_EVERY_CACHED_R1 1
+#endif
+template <typename T, bool NT>
+constexpr int kFlatEveryRows =
+  (sizeof(T) == 8 && !NT && ST_EVERY_CACHED_R1) ? 1 : kFlatRows;
+
+template <typename T, bool NT>
+inline uint32_t
+flat_every_tile(uint32_t nrows, uint32_t ncols)
+{
+  if (NT)
+    return 4u;
+  if (sizeof(T) == 4 || !ST_EVERY_CACHED_R1)
+    return 0u;
+  return block_bytes(nrows, ncols, sizeof(T)) >= ((size_t)384 << 20) ? 8u : 4u;
+}
+
 // partial sums per row (one per piece) and the scratch they need
 inline uint32_t
 flat_pieces(uint32_t ncols, int w)
@@ -513,22 +547,19 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
                   st_state* st, hipStream_t stream)
 {
   constexpr int U = kFlatU<T, W, NT>;
+  // rows per workgroup: 2, one on cached fp64 blocks (below)
+  constexpr int R = kFlatEveryRows<T, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
-  const uint32_t grid = (nrows + kFlatRows - 1) / kFlatRows * ppr;
+  const uint32_t grid = (nrows + R - 1) / R * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   const FlatGrid fg = flat_grid(grid);
-  // non-temporal blocks walk the pieces in tiles of 4 row groups
-  // (FlatPending::pt; tools/flat_map_sweep FMS_EVERY=1,
-  // profiles/r02_flat_map_every_*.log: 32768^2 fp64 2.625 vs 2.688 ms, fp32
-  // 1.301 vs 1.336, 16384 / 8192 x 65536 -1.8 / -1.0 %); cached blocks keep
-  // the row-major order (8192^2 fp64: tiles 0.7 % slower)
   dev::FlatPending<T, -1> pe{};
-  pe.pt = NT ? 4u : 0u;
+  pe.pt = flat_every_tile<T, NT>(nrows, ncols);
   if constexpr (kFlatFusedStats) {
     // two launches: m_k / stop_k folded into k_flat's first row group, the
     // v update into k_parts
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 0,
+      (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,
                    dev::kGatePlain, -1, U>),
       fg.grid,
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
@@ -541,7 +572,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, false, kFlatAlt, kBlock, 0,
+      (dev::k_flat<T, W, ORDER, NT, R, false, false, kFlatAlt, kBlock, 0,
                    dev::kGatePlain, -1, U>),
       fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
       row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
