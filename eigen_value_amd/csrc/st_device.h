@@ -1345,16 +1345,23 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   // v != nullptr: also v[r] *= s_k[r] / m_k (cpp:260) with m_k published by
   // k_flat's first row group
   // inv_next != nullptr (deferred writes): also 1 / s_{k+1}[r]
-  {
-    const uint32_t e =
-      __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (e != 0 && e <= k)
-      return;
-  }
+  // Every load is issued before the gate is tested (they are in bounds
+  // whatever the gate says; only the stores depend on it), so the launch
+  // waits for one memory round trip after its arguments instead of three
+  // in a row: the gate, the partials, then m_k / s_k / v.  The gate is a
+  // plain (scalar) load, as in k_flat (flat_gated): `end` only changes
+  // inside the k_flat launch before this one.
   const uint32_t r = (blockIdx.x * BLK + threadIdx.x) >> 6;
   const uint32_t lane = threadIdx.x & 63;
   if (r >= nrows)
     return; // whole waves leave together
+  const uint32_t e = state->end;
+  T vr = (T)0, sr = (T)1, m = (T)1;
+  if (v != nullptr && lane == 0) {
+    vr = v[row0 + r];
+    sr = s_cur[row0 + r];
+    m = (T)state->max;
+  }
   const T* row = part + (size_t)r * ppr;
   T acc = (T)0;
   for (uint32_t p = lane; p < ppr; p += 64)
@@ -1368,14 +1375,14 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
       acc2 += row2[p];
     acc += wave_sum(acc2);
   }
+  if (e != 0 && e <= k)
+    return;
   if (lane == 0) {
     s_next[r] = acc;
     if (inv_next != nullptr)
       inv_next[r] = (T)1 / acc;
-    if (v != nullptr) {
-      const T m = (T)state->max;
-      v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
-    }
+    if (v != nullptr)
+      v[row0 + r] = vr * (sr / m); // cpp:260
   }
 }
 

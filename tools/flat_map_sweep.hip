@@ -49,6 +49,7 @@ static std::vector<unsigned> g_pts = { 0, 16 };
 static int g_store_np = 3; // FMS_STORE_NP: the pending count of the storing round
 static int g_max_np = 3;   // FMS_MAX_NP (<= 5)
 static bool g_r8 = false;  // FMS_R8=1: 8 rows per workgroup instead of 2 and 4
+static bool g_r1 = false;  // FMS_R1=1: 1 and 2 rows per workgroup (every NP)
 static bool g_every = false; // FMS_EVERY=1: the every-round launch (NP = -1) only,
                              // R = 1, 2, 4 by PT
 
@@ -206,6 +207,14 @@ run(unsigned nr, unsigned n)
       by_pt<T, false, 2, -1>(b);
       by_pt<T, false, 4, -1>(b);
     }
+  } else if (g_r1) {
+    if (nt) {
+      by_np<T, true, 1>(b);
+      by_np<T, true, 2>(b);
+    } else {
+      by_np<T, false, 1>(b);
+      by_np<T, false, 2>(b);
+    }
   } else if (g_r8) {
     if (nt) {
       by_np<T, true, 4>(b);
@@ -244,6 +253,7 @@ main(int argc, char** argv)
   if (const char* e = std::getenv("FMS_MAX_NP"))
     g_max_np = std::atoi(e);
   g_r8 = std::getenv("FMS_R8") != nullptr;
+  g_r1 = std::getenv("FMS_R1") != nullptr;
   g_every = std::getenv("FMS_EVERY") != nullptr;
   if (const char* e = std::getenv("FMS_PT")) { // e.g. FMS_PT=0,4,8,16,32
     g_pts.clear();
