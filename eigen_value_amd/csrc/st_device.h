@@ -1111,17 +1111,38 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
   // then the row scales (vector loads, ld_row): s_k[r], or with deferred
   // writes already 1 / s_k[r], and the pending rounds' 1 / s_i[r]
+  // A whole row group (every group but a ragged last one) loads its R
+  // scales of a vector without per-row conditions, so that the scalar loads
+  // of adjacent rows merge (s_load_dwordx4 ... x16: one load and one address
+  // per vector instead of R).  fp64 rounds with 1 - 4 pending scalings only
+  // (tools/flat_map_sweep A/B, profiles/r02_rowload_merge_ab*.log: 32768^2
+  // NP = 4, 8 rows, tiles of 16: 1.23 vs 1.29 ms; the storing round with 5
+  // pending and fp32 lose 1 - 2 %, their merged scales crowd the SGPRs)
+  const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
+  constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && NP <= 4;
+  if (kMergeRows && r0 + R <= nrows) { // uniform
 #pragma unroll
-  for (int j = 0; j < R; j++) {
-    const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
-    sr[j] = r0 + j < nrows ? ld_row(rs + row0 + r0 + j) : (T)1;
-  }
-  if constexpr (NP > 0) {
+    for (int j = 0; j < R; j++)
+      sr[j] = ld_row(rs + row0 + r0 + j);
+    if constexpr (NP > 0) {
 #pragma unroll
-    for (int i = 0; i < NP; i++) {
+      for (int i = 0; i < NP; i++) {
 #pragma unroll
-      for (int j = 0; j < R; j++)
-        sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
+        for (int j = 0; j < R; j++)
+          sp_r[i][j] = ld_row(pend.inv[i] + row0 + r0 + j);
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < R; j++)
+      sr[j] = r0 + j < nrows ? ld_row(rs + row0 + r0 + j) : (T)1;
+    if constexpr (NP > 0) {
+#pragma unroll
+      for (int i = 0; i < NP; i++) {
+#pragma unroll
+        for (int j = 0; j < R; j++)
+          sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
+      }
     }
   }
   if constexpr (GATE == kGateSpec) {

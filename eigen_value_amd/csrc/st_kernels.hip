@@ -681,9 +681,12 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 //                     on non-temporal blocks, 16 on cached ones
 //   NP = 3, 4         8 rows (the column scales of 3 - 4 pending rounds then
 //                     serve 8 rows: 3-10 % over 4 rows, NP = 4 at 32768^2
-//                     fp64 1.230 vs 1.351 ms); row-major on non-temporal
-//                     blocks, tiled by 16 on cached ones
-//                     (profiles/r02_flat_map_r8_*.log)
+//                     fp64 1.230 vs 1.351 ms, profiles/r02_flat_map_r8_*.log),
+//                     tiled by 16: on non-temporal blocks the row-major
+//                     order's time depends on the allocation (32768^2 fp64
+//                     NP = 3 1.25 or 1.33 ms from one allocation to the
+//                     next, tiles of 16 1.20-1.22 in both;
+//                     profiles/r02_rowload_merge_ab*.log)
 //   storing rounds    row-major; 4 rows (10-16 % over 2), 8 on non-temporal
 //                     blocks when rounds are pending (3 %: 32768^2 fp64
 //                     2.852 vs 2.931 ms, 8192 x 65536 1.434 vs 1.481)
@@ -711,7 +714,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 #endif
   constexpr int kR0 = NT ? 2 : ST_DEFER_R0_CACHED;
   constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED;
-  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = NT ? 0u : 16u;
+  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
   // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
   // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
   constexpr int kRS = NT ? 8 : 4;
