@@ -36,7 +36,9 @@ Extra objects on the JSON line:
                    rows_per_gpu = 65536/N, one all-gather per round, checked
                    against the oracle's solve and the P = 1 count
   configs3_p1      (N = 1) the same matrix on one GPU: the strong-scaling
-                   anchor (also `configs3_p1_ms_per_iteration`)
+                   anchor (also `configs3_p1_ms_per_iteration`), and
+                   `rank_blocks`: rank 0's block at P = 2, 4, 8 timed alone
+                   (no all-gather) - the compute side of the curve
   north_star       (N = 1) 32768^2 random fp64, both forms
   configs4_f32     (N = 1) 32768^2 random fp32: every-round roofline, the
                    deferred-write rounds, the fp32-vs-fp64 tolerance study
@@ -424,7 +426,43 @@ def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representativ
     sh.close()
     del sh, v
     torch.cuda.empty_cache()
+    if world == 1:
+        leg["rank_blocks"] = rank_block_legs(sharded, torch, n, steps, warmup, representative)
     return leg
+
+
+def rank_block_legs(sharded, torch, n, steps, warmup, representative):
+    """configs[3]'s per-rank work at P = 2, 4, 8 on this one GPU: rank 0's
+    row block (n/P rows x n columns) through the same round launches a rank
+    runs - every-round steps and whole store cycles of the deferred-write
+    solve - WITHOUT the all-gather (the other ranks' row sums stay 1.0): the
+    compute side of the strong-scaling curve, not a multi-GPU measurement."""
+    out = {}
+    for P in (2, 4, 8):
+        sh = sharded.ShardedSimilarityTransform(n, torch.float64, rank_block=(P, 0))
+        p = sh.part
+        sh.load("random", seed=0)
+        el, fused = timed_rounds(sh, steps, warmup, torch, None, 1)
+        by = 2.0 * p.nrows * n * 8
+        r = {"rows": p.nrows, "cols": n, "block_gib": round(p.nrows * n * 8 / 2 ** 30, 2),
+             "ms_per_iteration": round(el / steps * 1e3, 4), "kernel_ms_avg": round(fused, 4),
+             "achieved": round(rate(by, fused), 1)}
+        if representative:
+            r["frac"] = round(rate(by, fused) / HBM_PEAK_GBS, 4)
+        if sh.deferred_writes:
+            _, ev_d, m = timed_deferred(sh, 4, 1, torch, None, 1)
+            by_d = (m + 1.0) / m * p.nrows * n * 8
+            r["deferred_writes"] = {"stores_every": m, "ms_per_iteration": round(ev_d, 4),
+                                    "achieved": round(rate(by_d, ev_d), 1)}
+            if representative:
+                r["deferred_writes"]["frac"] = round(rate(by_d, ev_d) / HBM_PEAK_GBS, 4)
+        out[f"P{P}"] = r
+        sh.close()
+        del sh
+        torch.cuda.empty_cache()
+    out["note"] = ("one rank's row block on one GPU, no all-gather (the other ranks' row sums "
+                   "held at 1.0): per-GPU compute of configs[3] at P = 2, 4, 8")
+    return out
 
 
 def deferred_leg(sharded, dev, torch, kind, n, dt, seed, every_ms):

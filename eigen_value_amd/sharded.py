@@ -226,22 +226,32 @@ class ShardedSimilarityTransform:
 
     def __init__(self, n: int, dtype=None, group=None, ops=None,
                  semantics: int = _lib.ST_SEM_SYCL, matrix_free: bool = False,
-                 comm: str = "auto", overlap: bool = False, deferred_writes: bool = True):
+                 comm: str = "auto", overlap: bool = False, deferred_writes: bool = True,
+                 rank_block: Optional[tuple] = None):
         import torch
         import torch.distributed as dist
         self.torch, self.dist, self.group = torch, dist, group
         self.dtype = dtype or torch.float64
         self.n = n
         self.semantics = semantics
-        world = dist.get_world_size(group) if dist.is_initialized() else 1
-        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        # rank_block = (P, p) without a process group: ONE rank's block of a
+        # P-way partition on this process, with no exchange - the row sums of
+        # the other ranks' slots stay 1.0 - for timing a rank's compute alone
+        # (bench.py configs3 rank blocks); its results are not the solve's
+        self.rehearsal = rank_block is not None
+        if self.rehearsal and dist.is_initialized():
+            raise ValueError("rank_block is for a process without a process group")
+        world = (rank_block[0] if self.rehearsal else
+                 dist.get_world_size(group) if dist.is_initialized() else 1)
+        rank = (rank_block[1] if self.rehearsal else
+                dist.get_rank(group) if dist.is_initialized() else 0)
         self.part = row_block(n, world, rank)
         if row_block(n, world, world - 1).nrows == 0:
             raise ValueError(f"n={n} leaves a rank of {world} without rows")
         self.ops = ops or HipShardOps()
         p = self.part
         self.matrix_free = matrix_free
-        self.s = [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(2)]
+        self.s = [self._vec() for _ in range(2)]
         self.vb = [self.ops.empty((p.world * p.chunk,), self.dtype)
                    for _ in range(2 if matrix_free else 1)]
         self.v = self.vb[0]
@@ -268,7 +278,8 @@ class ShardedSimilarityTransform:
         self.rccl = None
         if comm not in ("auto", "native", "torch"):
             raise ValueError(f"comm must be auto, native or torch, not {comm!r}")
-        if world > 1 and comm != "torch" and isinstance(self.ops, HipShardOps) \
+        if world > 1 and not self.rehearsal and comm != "torch" \
+                and isinstance(self.ops, HipShardOps) \
                 and dist.get_backend(group) == "nccl":
             try:
                 self.rccl = RcclComm(group)
@@ -278,6 +289,15 @@ class ShardedSimilarityTransform:
                 import warnings
                 warnings.warn(f"library RCCL communicator unavailable ({e}); "
                               "using torch.distributed all_gather_into_tensor")
+
+    def _vec(self):
+        """A padded P*chunk row-sum vector (1.0 everywhere in a rank_block
+        rehearsal, whose other slots are never gathered)."""
+        p = self.part
+        x = self.ops.empty((p.world * p.chunk,), self.dtype)
+        if self.rehearsal:
+            self.ops.fill(x, 1.0)
+        return x
 
     def close(self) -> None:
         """Release the library's RCCL communicator (after the stream drained;
@@ -311,7 +331,7 @@ class ShardedSimilarityTransform:
     def gather(self, s):
         """All-gather the padded per-rank slots of s (one RCCL call)."""
         p = self.part
-        if p.world > 1:
+        if p.world > 1 and not self.rehearsal:
             slot = s[p.rank * p.chunk:(p.rank + 1) * p.chunk]
             if self.rccl is not None:
                 self.rccl.allgather(s, slot)
@@ -396,8 +416,8 @@ class ShardedSimilarityTransform:
         p = self.part
         m = self.ops.defer_rounds(p.nrows, p.n, self.dtype)
         if self._ring is None or len(self._ring[0]) != m + 1:
-            self._ring = ([self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(m + 1)],
-                          [self.ops.empty((p.world * p.chunk,), self.dtype) for _ in range(m + 1)])
+            self._ring = ([self._vec() for _ in range(m + 1)],
+                          [self._vec() for _ in range(m + 1)])
         return m
 
     def _pending(self, j0: int, count: int):

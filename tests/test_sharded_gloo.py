@@ -395,3 +395,30 @@ def test_sharded_deferred_writes_bit_identical_to_oracle(tmp_path, orc, world, n
         assert np.array_equal(np.load(tmp_path / f"a{r}.npy"), a_end[row0:row0 + nrows])
     if policy == "uneven":
         assert saw_defer and saw_plain
+
+
+def test_rank_block_rehearsal_without_a_group(orc):
+    """rank_block=(P, p) (bench.py's configs[3] rank blocks): one rank's
+    block of a P-way partition in a process with no process group, no
+    exchange and no communicator; the other ranks' row sums stay 1.0, so a
+    round transforms the block with s = [1 .. own row sums .. 1] - the
+    every-round and the deferred-write loops both run."""
+    assert not dist.is_initialized()
+    n, P, p = 90, 3, 1
+    sh = ShardedSimilarityTransform(n, torch.float64, ops=CpuShardOps(), rank_block=(P, p))
+    b = sh.part
+    assert (b.world, b.rank, b.row0, b.nrows) == (3, 1, 30, 30) and sh.rccl is None
+    a0 = sh.load("random", seed=3).numpy().copy()
+    sh.start()
+    sh.round(0.0, 1000)
+    s = np.ones(b.world * b.chunk)
+    s[b.row0:b.row0 + b.nrows] = orc.rowsum(a0)
+    assert np.array_equal(sh.mat.numpy(), orc.compute_next(a0, s[:n], row0=b.row0, order=0))
+    ops = CpuDeferOps()
+    sd = ShardedSimilarityTransform(n, torch.float64, ops=ops, rank_block=(P, p))
+    sd.load("random", seed=3)
+    assert sd.deferred_writes
+    sd.deferred_start()
+    for _ in range(2 * sd._defer_m):
+        sd.deferred_round(0.0, 1000)
+    assert ops.stores == 2
