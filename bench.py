@@ -39,6 +39,8 @@ Extra objects on the JSON line:
                    anchor (also `configs3_p1_ms_per_iteration`), and
                    `rank_blocks`: rank 0's block at P = 2, 4, 8 timed alone
                    (no all-gather) - the compute side of the curve
+  weak_rank_blocks (N = 1) rank 0's block of the N = 2, 4, 8 headline
+                   timed alone (no all-gather)
   north_star       (N = 1) 32768^2 random fp64, both forms
   configs4_f32     (N = 1) 32768^2 random fp32: every-round roofline, the
                    deferred-write rounds, the fp32-vs-fp64 tolerance study
@@ -427,21 +429,26 @@ def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representativ
     del sh, v
     torch.cuda.empty_cache()
     if world == 1:
-        leg["rank_blocks"] = rank_block_legs(sharded, torch, n, steps, warmup, representative)
+        leg["rank_blocks"] = rank_block_legs(sharded, torch, [(P, n) for P in (2, 4, 8)],
+                                             "random", steps, warmup, representative)
+        leg["rank_blocks"]["note"] = (
+            "one rank's row block on one GPU, no all-gather (the other ranks' row sums held at "
+            "1.0): per-GPU compute of configs[3] at P = 2, 4, 8")
     return leg
 
 
-def rank_block_legs(sharded, torch, n, steps, warmup, representative):
-    """configs[3]'s per-rank work at P = 2, 4, 8 on this one GPU: rank 0's
-    row block (n/P rows x n columns) through the same round launches a rank
-    runs - every-round steps and whole store cycles of the deferred-write
-    solve - WITHOUT the all-gather (the other ranks' row sums stay 1.0): the
-    compute side of the strong-scaling curve, not a multi-GPU measurement."""
+def rank_block_legs(sharded, torch, cases, kind, steps, warmup, representative):
+    """Per-rank work of a P-way row-block partition on this one GPU, for
+    each (P, n) in `cases`: rank 0's block (ceil(n/P) rows x n columns)
+    through the same round launches a rank runs - every-round steps and
+    whole store cycles of the deferred-write solve - WITHOUT the all-gather
+    (the other ranks' row sums stay 1.0): the compute side of a scaling
+    curve, not a multi-GPU measurement."""
     out = {}
-    for P in (2, 4, 8):
+    for P, n in cases:
         sh = sharded.ShardedSimilarityTransform(n, torch.float64, rank_block=(P, 0))
         p = sh.part
-        sh.load("random", seed=0)
+        sh.load(kind, seed=0)
         el, fused = timed_rounds(sh, steps, warmup, torch, None, 1)
         by = 2.0 * p.nrows * n * 8
         r = {"rows": p.nrows, "cols": n, "block_gib": round(p.nrows * n * 8 / 2 ** 30, 2),
@@ -460,8 +467,6 @@ def rank_block_legs(sharded, torch, n, steps, warmup, representative):
         sh.close()
         del sh
         torch.cuda.empty_cache()
-    out["note"] = ("one rank's row block on one GPU, no all-gather (the other ranks' row sums "
-                   "held at 1.0): per-GPU compute of configs[3] at P = 2, 4, 8")
     return out
 
 
@@ -781,6 +786,18 @@ def main():
     mf.close()
     del mf
 
+    # ---- N = 1: the weak-scaled headline's per-GPU blocks at N = 2, 4, 8 --
+    # (rank 0's block of n = 8192*sqrt(N), timed alone: the compute side of
+    # the driver's 1 -> 8 weak-scaling curve; the all-gather is not in it)
+    weak_blocks = None
+    if world == 1 and not args.strong and args.dtype == "f64":
+        weak_blocks = rank_block_legs(sharded, torch,
+                                      [(P, scaled_n(args.n, P)) for P in (2, 4, 8)],
+                                      args.kind, args.steps, args.warmup, representative)
+        weak_blocks["note"] = ("rank 0's block of the weak-scaled headline (n = "
+                               f"{args.n}*sqrt(N)) on one GPU, no all-gather; ~512 MiB blocks, "
+                               "memory-side-cache assisted like the N = 1 line")
+
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
            "warmup": args.warmup, "ms_per_step": round(el / args.steps * 1e3, 5),
@@ -801,6 +818,8 @@ def main():
         out["rccl_ranks"] = exchange["rccl_ranks"]
     if overlap_leg is not None:
         out["exchange_overlap"] = overlap_leg
+    if weak_blocks is not None:
+        out["weak_rank_blocks"] = weak_blocks
     sh.close()
     del sh
     torch.cuda.empty_cache()
