@@ -117,7 +117,7 @@ one(const Block<T>& b, unsigned pt)
   });
   const double bytes = (store ? 2.0 : 1.0) * b.nr * (double)b.n * sizeof(T);
   std::printf("  NP=%2d R=%d PT=%5u nt=%d%s  %8.4f ms  %7.1f GB/s\n", NP, R, pt, (int)NT,
-              UF ? (UF == 2 ? " U=2" : " U=4") : "", ms, bytes / (ms * 1e-3) / 1e9);
+              UF ? (UF == 1 ? " U=1" : UF == 2 ? " U=2" : " U=4") : "", ms, bytes / (ms * 1e-3) / 1e9);
   std::fflush(stdout);
 }
 
@@ -202,6 +202,10 @@ run(unsigned nr, unsigned n)
       by_pt<T, true, 1, -1>(b);
       by_pt<T, true, 2, -1>(b);
       by_pt<T, true, 4, -1>(b);
+    } else if (std::getenv("FMS_U1")) { // 4 KB pieces on a cached fp64 block
+      by_pt<T, false, 1, -1>(b);
+      by_pt<T, false, 1, -1, 1>(b);
+      by_pt<T, false, 2, -1, 1>(b);
     } else {
       by_pt<T, false, 1, -1>(b);
       by_pt<T, false, 2, -1>(b);
