@@ -101,6 +101,8 @@ def parse(argv=None):
                         "second stream) as the headline instead of an extra leg")
     p.add_argument("--no-overlap-leg", action="store_true",
                    help="N > 1: skip the extra overlapped-exchange leg")
+    p.add_argument("--leg", default=None, help=argparse.SUPPRESS)   # child mode
+    p.add_argument("--leg-args", default="{}", help=argparse.SUPPRESS)
     p.add_argument("--one-gpu", action="store_true",
                    help="rehearsal: every rank on cuda:0 (use with --backend gloo); the "
                         "line is marked non-representative")
@@ -274,6 +276,7 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     every 175 us round).  With N > 1 the all-gathers sit between launches:
     the timed region runs without events, and a separate pass after it
     brackets each launch with its own pair for the kernel average."""
+    cool_down(torch)
     sh.start()
     for _ in range(warmup):
         sh.round(0.0, BIG)
@@ -312,6 +315,7 @@ def timed_deferred(sh, cycles, warm_cycles, torch, dist, world):
     after a store (no pending scaling) and ending on a storing round, no
     flush inside.  Returns (elapsed_s_max, event_ms_per_round, m) — HIP
     events bracket the cycles on the launch stream."""
+    cool_down(torch)
     sh.deferred_start()
     m = sh._defer_m
     for _ in range(warm_cycles * m):
@@ -379,6 +383,18 @@ def rate(bytes_, ms):
     return bytes_ / (ms * 1e-3) / 1e9
 
 
+COOL_S = float(os.environ.get("BENCH_COOL_S", "0"))
+
+
+def cool_down(torch):
+    """Idle before a leg's timed region (BENCH_COOL_S seconds): each leg
+    of a long bench starts from a comparable thermal state instead of
+    inheriting the clock the previous leg's streaming left behind."""
+    if COOL_S > 0:
+        torch.cuda.synchronize()
+        time.sleep(COOL_S)
+
+
 def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representative):
     """BASELINE configs[3]: 65536^2 random fp64 row-block sharded over the
     world (P = 1: the whole 32 GiB on one GPU), one all-gather per round:
@@ -428,12 +444,6 @@ def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representativ
     sh.close()
     del sh, v
     torch.cuda.empty_cache()
-    if world == 1:
-        leg["rank_blocks"] = rank_block_legs(sharded, torch, [(P, n) for P in (2, 4, 8)],
-                                             "random", steps, warmup, representative)
-        leg["rank_blocks"]["note"] = (
-            "one rank's row block on one GPU, no all-gather (the other ranks' row sums held at "
-            "1.0): per-GPU compute of configs[3] at P = 2, 4, 8")
     return leg
 
 
@@ -639,6 +649,138 @@ def cpu_leg(args, np_, workload, n, bytes_round_total, ms_per_step):
     return out
 
 
+def north_star_leg(sharded, dev, torch):
+    """32768^2 random fp64 on one GPU: the
+    reference-semantics solve (checked against the oracle's solve and the
+    Perron root) and 50 every-round steps (the matrix-free form: north_star_mf_leg)."""
+    ns = sharded.ShardedSimilarityTransform(32768, torch.float64)
+    ns.load("random", seed=0)
+    lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=1)
+    ns.load("random", seed=0)
+    el_ns, fused_ns = timed_rounds(ns, 50, 3, torch, None, 1)
+    by = 2.0 * 32768 * 32768 * 8
+    ach = rate(by, fused_ns)
+    flat_ns = dev.flat_round_pays(32768, 32768, torch.float64)
+    tr = load_traffic("random32768_f64", "k_flat" if flat_ns else "k_round")
+    out = {"workload": "random32768_f64",
+           "kernel": "flat round: k_flat + k_parts (round time)" if flat_ns else "k_round",
+           "ms_per_iteration": round(el_ns / 50 * 1e3, 4),
+           "fused_ms_avg": round(fused_ns, 4), "achieved": round(ach, 1),
+           "frac": round(ach / HBM_PEAK_GBS, 4), "target_frac": 0.70,
+           "traffic": None if tr is None else tr[0],
+           "solve_iter_count": it_ns, "eigen_val": lam_ns}
+    pin = true_lambda(32768, "f64", 0)
+    if pin is not None:  # CPU Perron root of the same matrix (tests/golden)
+        out["eigen_val_rel_err_vs_true"] = abs(lam_ns - pin) / pin
+    opin = oracle_pin("random32768_f64")
+    if opin is not None:  # the oracle's solve of the same matrix
+        out["check"] = {
+            "iter_count_equal_oracle": it_ns == opin["iter_count"],
+            "eigen_val_rel_err_vs_oracle": abs(lam_ns - opin["eigen_val"]) / opin["eigen_val"]}
+    ns.close()
+    del ns
+    torch.cuda.empty_cache()
+    return {"north_star": out, "every_ms": el_ns / 50 * 1e3}
+
+
+def north_star_mf_leg(sharded, torch, lam_ns):
+    """The matrix-free form on the north star's 32768^2 input (N^2*b per
+    round), λ against the transform's."""
+    mf = sharded.ShardedSimilarityTransform(32768, torch.float64, matrix_free=True)
+    mf.load("random", seed=0)
+    lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=1)
+    el_mf, k_mf = timed_rounds(mf, 50, 3, torch, None, 1)
+    by_mf = 1.0 * 32768 * 32768 * 8
+    tr_mf = load_traffic("random32768_f64", "k_mfree")
+    out = {
+        "traffic": None if tr_mf is None else tr_mf[0],
+        "ms_per_iteration": round(el_mf / 50 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
+        "achieved": round(rate(by_mf, k_mf), 1),
+        "frac": round(rate(by_mf, k_mf) / HBM_PEAK_GBS, 4),
+        "bytes_per_round": by_mf, "solve_iter_count": it_mf,
+        "eigen_val_rel_diff_vs_transform": abs(lam_mf - lam_ns) / lam_ns}
+    mf.close()
+    del mf
+    torch.cuda.empty_cache()
+    return {"matrix_free": out}
+
+
+def run_leg(name, a):
+    """One full-size N = 1 leg; `a` = the parent's shape arguments."""
+    import numpy as np
+    import torch
+
+    from eigen_value_amd import device as dev
+    from eigen_value_amd import sharded
+    if name == "north_star":
+        return north_star_leg(sharded, dev, torch)
+    if name == "north_star_mf":
+        return north_star_mf_leg(sharded, torch, a["lam_ns"])
+    if name == "configs4":
+        c4 = configs4_leg(sharded, dev, torch, np, None)
+        return {"configs4_f32": c4, "every_ms": c4.pop("_every_ms")}
+    if name == "deferred":
+        dt = torch.float64 if a["dtype"] == "f64" else torch.float32
+        name_, kind, nn, ddt, key = (
+            ("configs[1] " + f"{a['kind']}{a['n']}_{a['dtype']}", a["kind"], a["n"], dt,
+             f"{a['kind']}{a['n']}_{a['dtype']}"),
+            ("north_star random32768_f64", "random", 32768, torch.float64, "random32768_f64"),
+            ("configs[4] random32768_f32", "random", 32768, torch.float32, "random32768_f32"),
+        )[a["which"]]
+        leg = deferred_leg(sharded, dev, torch, kind, nn, ddt, 0, a["every_ms"][key])
+        return {"deferred_writes": {} if leg is None else {name_: leg}}
+    if name == "configs3":
+        return {"configs3_p1": configs3_leg(sharded, torch, None, 1, 0,
+                                            max(5, min(a["steps"], 20)), min(a["warmup"], 3),
+                                            a["representative"])}
+    if name == "rank_blocks":
+        rb = rank_block_legs(sharded, torch, [(P, 65536) for P in (2, 4, 8)], "random",
+                             max(5, min(a["steps"], 20)), min(a["warmup"], 3),
+                             a["representative"])
+        rb["note"] = ("one rank's row block on one GPU, no all-gather (the other ranks' row "
+                      "sums held at 1.0): per-GPU compute of configs[3] at P = 2, 4, 8")
+        return {"rank_blocks": rb}
+    raise ValueError(f"unknown leg {name}")
+
+
+LEG_TAG = "@@LEG "
+
+
+def child_leg(name, a):
+    """Run leg `name` in a fresh child process (`bench.py --leg`) and return
+    its result; if the child fails, run it in this process instead and say
+    so in the result (`in_process`)."""
+    import torch
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--leg", name, "--leg-args", json.dumps(a)]
+    err = None
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
+        for ln in reversed(r.stdout.splitlines()):
+            if ln.startswith(LEG_TAG):
+                return json.loads(ln[len(LEG_TAG):])
+        err = f"child exited {r.returncode}: {r.stderr[-400:]}"
+    except Exception as e:  # noqa: BLE001 - fall back below
+        err = repr(e)[:400]
+    res = run_leg(name, a)
+    res["in_process"] = err
+    return res
+
+
+def leg_main(args):
+    """--leg NAME: one full-size leg in this (child) process; prints its
+    result as one tagged JSON line."""
+    a = json.loads(args.leg_args)
+    import torch
+    torch.cuda.set_device(a["device"])
+    from eigen_value_amd import _lib
+    _lib.load()
+    print(LEG_TAG + json.dumps(run_leg(args.leg, a)), flush=True)
+
+
 def strip_fracs(obj):
     """Drop every roofline fraction (one-GPU rehearsals share one card)."""
     if isinstance(obj, dict):
@@ -651,6 +793,8 @@ def strip_fracs(obj):
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
+    if args.leg:
+        return leg_main(args)
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
         sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
@@ -824,88 +968,42 @@ def main():
     del sh
     torch.cuda.empty_cache()
 
-    # ---- north-star size: 32768^2 random fp64 on one GPU ---------------
-    every_ms = {}
+    # ---- N = 1: the full-size legs, each in a fresh child process --------
+    # (a block allocated after other multi-GiB blocks in the same process
+    # streams 1-2.5 % slower - tools/alloc_probe.py --pre,
+    # profiles/r02_alloc_probe_pre.log - so every full-size leg gets a
+    # process of its own, the way the driver's fresh N = 1 run gets its
+    # headline block; a child that fails is re-run here in-process)
     if world == 1 and full:
-        ns = sharded.ShardedSimilarityTransform(32768, torch.float64)
-        ns.load("random", seed=0)
-        lam_ns, _, it_ns, _ = ns.solve(eps=1e-3, max_itr=1000, batch=1)
-        ns.load("random", seed=0)
-        el_ns, fused_ns = timed_rounds(ns, 50, 3, torch, dist, 1)
-        by = 2.0 * 32768 * 32768 * 8
-        ach = rate(by, fused_ns)
-        flat_ns = dev.flat_round_pays(32768, 32768, torch.float64)
-        tr = load_traffic("random32768_f64", "k_flat" if flat_ns else "k_round")
-        every_ms["random32768_f64"] = el_ns / 50 * 1e3
-        out["north_star"] = {"workload": "random32768_f64",
-                             "kernel": ("flat round: k_flat + k_parts (round time)"
-                                        if flat_ns else "k_round"),
-                             "ms_per_iteration": round(el_ns / 50 * 1e3, 4),
-                             "fused_ms_avg": round(fused_ns, 4), "achieved": round(ach, 1),
-                             "frac": round(ach / HBM_PEAK_GBS, 4), "target_frac": 0.70,
-                             "traffic": None if tr is None else tr[0],
-                             "solve_iter_count": it_ns, "eigen_val": lam_ns}
-        pin = true_lambda(32768, "f64", 0)
-        if pin is not None:  # CPU Perron root of the same matrix (tests/golden)
-            out["north_star"]["eigen_val_rel_err_vs_true"] = abs(lam_ns - pin) / pin
-        opin = oracle_pin("random32768_f64")
-        if opin is not None:  # the oracle's solve of the same matrix
-            out["north_star"]["check"] = {
-                "iter_count_equal_oracle": it_ns == opin["iter_count"],
-                "eigen_val_rel_err_vs_oracle": abs(lam_ns - opin["eigen_val"]) / opin["eigen_val"]}
-        ns.close()
-        del ns
-        torch.cuda.empty_cache()
-        # the matrix-free form on the same 32768^2 input (N^2*b per round)
-        mf = sharded.ShardedSimilarityTransform(32768, torch.float64, matrix_free=True)
-        mf.load("random", seed=0)
-        lam_mf, _, it_mf, _ = mf.solve(eps=1e-3, max_itr=1000, batch=1)
-        el_mf, k_mf = timed_rounds(mf, 50, 3, torch, dist, 1)
-        by_mf = 1.0 * 32768 * 32768 * 8
-        tr_mf = load_traffic("random32768_f64", "k_mfree")
-        out["north_star"]["matrix_free"] = {
-            "traffic": None if tr_mf is None else tr_mf[0],
-            "ms_per_iteration": round(el_mf / 50 * 1e3, 4), "kernel_ms_avg": round(k_mf, 4),
-            "achieved": round(rate(by_mf, k_mf), 1),
-            "frac": round(rate(by_mf, k_mf) / HBM_PEAK_GBS, 4),
-            "bytes_per_round": by_mf, "solve_iter_count": it_mf,
-            "eigen_val_rel_diff_vs_transform": abs(lam_mf - lam_ns) / lam_ns}
-        mf.close()
-        del mf
-        torch.cuda.empty_cache()
-
-        # ---- configs[4]: 32768^2 fp32 ----------------------------------
-        c4 = configs4_leg(sharded, dev, torch, np, dist)
-        every_ms["random32768_f32"] = c4.pop("_every_ms")
-        out["configs4_f32"] = c4
-
-        # ---- deferred writes: the solve loop's form (flat blocks) -------
+        sh_args = {"device": dev_index, "steps": args.steps, "warmup": args.warmup,
+                   "kind": args.kind, "n": n, "dtype": args.dtype,
+                   "representative": representative}
+        ns = child_leg("north_star", sh_args)
+        out["north_star"] = ns["north_star"]
+        out["north_star"]["matrix_free"] = child_leg(
+            "north_star_mf", dict(sh_args, lam_ns=ns["north_star"]["eigen_val"]))["matrix_free"]
+        c4 = child_leg("configs4", sh_args)
+        out["configs4_f32"] = c4["configs4_f32"]
+        every_ms = {"random32768_f64": ns["every_ms"], "random32768_f32": c4["every_ms"],
+                    workload: el / args.steps * 1e3}
         deferred = {}
-        for name, kind, nn, ddt, key in (
-                ("configs[1] " + workload, args.kind, n, dt, None),
-                ("north_star random32768_f64", "random", 32768, torch.float64,
-                 "random32768_f64"),
-                ("configs[4] random32768_f32", "random", 32768, torch.float32,
-                 "random32768_f32")):
-            em = every_ms.get(key, el / args.steps * 1e3) if key else el / args.steps * 1e3
-            leg = deferred_leg(sharded, dev, torch, kind, nn, ddt, 0, em)
-            if leg is not None:
-                deferred[name] = leg
+        for i in range(3):
+            d = child_leg("deferred", dict(sh_args, which=i, every_ms=every_ms))
+            deferred.update(d["deferred_writes"])
         out["deferred_writes"] = deferred
         if "configs[4] random32768_f32" in deferred:
             out["configs4_f32"]["deferred_writes"] = deferred["configs[4] random32768_f32"]
+        if not args.no_configs3:
+            c3 = child_leg("configs3", sh_args)["configs3_p1"]
+            c3["rank_blocks"] = child_leg("rank_blocks", sh_args)["rank_blocks"]
+            out["configs3_p1"] = c3
+            out["configs3_p1_ms_per_iteration"] = c3["ms_per_iteration"]
 
-    # ---- configs[3]: 65536^2 fp64, strong-scaled over the world ----------
-    # (after the 32768^2 legs at N = 1: its minutes of full-chip streaming
-    # warm the chip, which then clocks ~1 % lower for the legs that follow)
-    if not args.no_configs3 and (world > 1 or full):
-        leg = configs3_leg(sharded, torch, dist, world, rank, max(5, min(args.steps, 20)),
-                           min(args.warmup, 3), representative)
-        if world > 1:
-            out["configs3_strong"] = leg
-        else:
-            out["configs3_p1"] = leg
-            out["configs3_p1_ms_per_iteration"] = leg["ms_per_iteration"]
+    # ---- N > 1: configs[3] strong-scaled over the world ------------------
+    if world > 1 and not args.no_configs3:
+        out["configs3_strong"] = configs3_leg(sharded, torch, dist, world, rank,
+                                              max(5, min(args.steps, 20)),
+                                              min(args.warmup, 3), representative)
 
     # ---- the reference's own headline, apples to apples ----------------
     # README.md:66-158 of the reference publishes whole solves of the fp32

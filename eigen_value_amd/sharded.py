@@ -74,6 +74,10 @@ class HipShardOps:
         return self.dev.generate(kind, n, dtype=dtype, nrows=nrows, row0=row0,
                                  seed=seed, device=self.device)
 
+    def generate_into(self, kind, n, row0, seed, out):
+        self.dev.generate(kind, n, dtype=out.dtype, nrows=out.shape[0], row0=row0,
+                          seed=seed, device=self.device, out=out)
+
     def new_state(self):
         return self.dev.new_state(self.device)
 
@@ -319,11 +323,18 @@ class ShardedSimilarityTransform:
         return s[p.rank * p.chunk:p.rank * p.chunk + p.nrows]
 
     def load(self, kind: str = "hilbert", seed: int = 0, mat=None):
-        """Generate (or adopt) this rank's row block."""
+        """Generate (or adopt) this rank's row block.  A block already held
+        is regenerated in place where the ops can (no second multi-GiB
+        allocation: one made after others in a process streams 1-2.5 %
+        slower, profiles/r02_alloc_probe_pre.log); the returned tensor is
+        then the same one."""
         p = self.part
         if mat is not None:
             assert tuple(mat.shape) == (p.nrows, p.n)
             self.mat = mat
+        elif self.mat is not None and hasattr(self.ops, "generate_into") \
+                and tuple(self.mat.shape) == (p.nrows, p.n) and self.mat.dtype == self.dtype:
+            self.ops.generate_into(kind, p.n, p.row0, seed, self.mat)
         else:
             self.mat = self.ops.generate(kind, p.n, self.dtype, p.nrows, p.row0, seed)
         return self.mat

@@ -19,10 +19,17 @@ def main():
     ap.add_argument("--reps", type=int, default=6)
     ap.add_argument("--dtype", default="f64")
     ap.add_argument("--keep", type=int, default=1, help="keep previous blocks alive")
+    ap.add_argument("--pre", default="", help="comma-separated sizes to generate and free "
+                                               "first (torch.cuda.empty_cache after each)")
     a = ap.parse_args()
     import torch
     from eigen_value_amd import device as dev
     dt = torch.float64 if a.dtype == "f64" else torch.float32
+    for m in [int(x) for x in a.pre.split(",") if x]:
+        t = dev.generate("random", m, dt, seed=0, device="cuda")
+        torch.cuda.synchronize()
+        del t
+        torch.cuda.empty_cache()
     n, K = a.n, 20
     held = []
     s = 1.0 + 1e-6 * torch.rand(n, dtype=dt, device="cuda")
