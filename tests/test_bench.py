@@ -107,3 +107,21 @@ def test_bench_self_spawned_two_ranks_on_one_gpu():
     assert c3["solve"]["check"]["iter_count_equal"] is True
     assert c3["solve"]["check"]["eigen_val_rel_err_vs_oracle"] <= 1e-10
     assert d["exchange"]["backend"] == "gloo" and d["rccl_ranks"] is None
+
+
+@pytest.mark.gpu
+def test_bench_leg_child_mode():
+    """`bench.py --leg NAME --leg-args JSON` (how the N = 1 line runs each
+    full-size leg in a fresh process): the configs[1] deferred-write leg
+    prints one tagged JSON line, bitwise equal to storing every round."""
+    a = {"device": 0, "steps": 5, "warmup": 1, "kind": "hilbert", "n": 8192, "dtype": "f64",
+         "representative": True, "which": 0, "every_ms": {"hilbert8192_f64": 0.157}}
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--leg", "deferred",
+                          "--leg-args", json.dumps(a)],
+                         capture_output=True, text=True, timeout=600, cwd=REPO)
+    assert out.returncode == 0, out.stderr[-4000:]
+    tagged = [ln for ln in out.stdout.splitlines() if ln.startswith(bench.LEG_TAG)]
+    assert len(tagged) == 1 and not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    leg = json.loads(tagged[0][len(bench.LEG_TAG):])["deferred_writes"]["configs[1] hilbert8192_f64"]
+    assert leg["bitwise_equal_to_write_every_round"] is True and leg["stores_every"] == 6
+    assert 0 < leg["ms_per_iteration"] < 0.157
