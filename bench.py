@@ -733,6 +733,13 @@ def run_leg(name, a):
         return {"configs3_p1": configs3_leg(sharded, torch, None, 1, 0,
                                             max(5, min(a["steps"], 20)), min(a["warmup"], 3),
                                             a["representative"])}
+    if name == "weak_rank_blocks":
+        wb = rank_block_legs(sharded, torch, [(P, scaled_n(a["n"], P)) for P in (2, 4, 8)],
+                             a["kind"], a["steps"], a["warmup"], a["representative"])
+        wb["note"] = ("rank 0's block of the weak-scaled headline (n = "
+                      f"{a['n']}*sqrt(N)) on one GPU, no all-gather; ~512 MiB blocks, "
+                      "memory-side-cache assisted like the N = 1 line")
+        return {"weak_rank_blocks": wb}
     if name == "rank_blocks":
         rb = rank_block_legs(sharded, torch, [(P, 65536) for P in (2, 4, 8)], "random",
                              max(5, min(a["steps"], 20)), min(a["warmup"], 3),
@@ -933,14 +940,14 @@ def main():
     # ---- N = 1: the weak-scaled headline's per-GPU blocks at N = 2, 4, 8 --
     # (rank 0's block of n = 8192*sqrt(N), timed alone: the compute side of
     # the driver's 1 -> 8 weak-scaling curve; the all-gather is not in it)
+    # (a child process too, so that a profile of this process holds the
+    # headline's launches only)
     weak_blocks = None
     if world == 1 and not args.strong and args.dtype == "f64":
-        weak_blocks = rank_block_legs(sharded, torch,
-                                      [(P, scaled_n(args.n, P)) for P in (2, 4, 8)],
-                                      args.kind, args.steps, args.warmup, representative)
-        weak_blocks["note"] = ("rank 0's block of the weak-scaled headline (n = "
-                               f"{args.n}*sqrt(N)) on one GPU, no all-gather; ~512 MiB blocks, "
-                               "memory-side-cache assisted like the N = 1 line")
+        weak_blocks = child_leg("weak_rank_blocks", {
+            "device": dev_index, "steps": args.steps, "warmup": args.warmup,
+            "kind": args.kind, "n": args.n, "dtype": args.dtype,
+            "representative": representative})["weak_rank_blocks"]
 
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
