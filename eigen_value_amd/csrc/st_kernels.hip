@@ -690,8 +690,8 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 //   storing rounds    row-major; 4 rows (10-16 % over 2), 8 on non-temporal
 //                     blocks when rounds are pending (3 %: 32768^2 fp64
 //                     2.852 vs 2.931 ms, 8192 x 65536 1.434 vs 1.481)
-// (the every-round flat round keeps 2 rows, row-major: the tiled order
-// and 4 rows lose 2-4 % there)
+// (the every-round flat round has its own shapes: kFlatEveryRows /
+// flat_every_tile above)
 template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
