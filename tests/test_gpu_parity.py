@@ -161,7 +161,10 @@ def test_round_kernel_vs_oracle(orc, dt, sem, nrows, ncols, row0):
 @pytest.mark.parametrize("dt", [np.float64, np.float32])
 @pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
 @pytest.mark.parametrize("nrows,ncols,row0", [(1, 1, 0), (3, 3, 0), (7, 257, 100), (1025, 2048, 1000),
-                                              (2049, 3000, 0), (1500, 1501, 0)])
+                                              (2049, 3000, 0), (1500, 1501, 0),
+                                              # fp64: >= 384 MiB, the every-round launch's
+                                              # tiles of 8 rows, a ragged last tile
+                                              (6203, 8192, 0)])
 def test_flat_round_vs_round(orc, dt, sem, nrows, ncols, row0):
     """st_round_flat_* (k_stats + k_flat + k_parts) against st_round_* and the
     oracle: A_{k+1} and v bit for bit, the state identical, s_{k+1} to
@@ -1054,6 +1057,7 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 # bit-identical λ, v, iteration count, row-sum bookkeeping and final matrix
 # ---------------------------------------------------------------------------
 @pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144),
+                                  (np.float64, 8192),    # configs[1]: 1-row tiles of 8
                                   (np.float64, 4353),    # odd: element-wide access
                                   # just past 2 GiB: non-temporal, 4 rounds per
                                   # store, element-wide (n % 16 B != 0)
