@@ -717,7 +717,16 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
   // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
   // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
+#ifndef ST_DEFER_STORE_R8_CACHED // A/B probe switch
+#define ST_DEFER_STORE_R8_CACHED 1
+#endif
+  // cached fp64 blocks: 8 rows tiled by 4 for the storing round with 5
+  // pending (8192^2 0.160 vs 0.165 ms, the P = 8 block level;
+  // profiles/r02_flat_map_r8_f64_cached_store5.log)
+  constexpr bool kS8 = !NT && sizeof(T) == 8 && ST_DEFER_STORE_R8_CACHED;
   constexpr int kRS = NT ? 8 : 4;
+  constexpr int kRS5 = kS8 ? 8 : kRS;
+  constexpr uint32_t kTileS5 = kS8 ? 4u : 0u;
   constexpr int kR2 = NT ? 8 : 4; // NP = 2: 1-2 % with 8 rows, non-temporal only
   static_assert(kDeferRoundsMax == 6, "one case per pending count below");
   if (store) {
@@ -727,7 +736,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
     case 2: ST_NP(2, kRS, 0u); break;
     case 3: ST_NP(3, kRS, 0u); break;
     case 4: ST_NP(4, kRS, 0u); break;
-    default: ST_NP(5, kRS, 0u); break;
+    default: ST_NP(5, kRS5, kTileS5); break;
     }
   } else {
     switch (npend) {
