@@ -707,13 +707,19 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, store, flush, PTV, stream)
 #ifndef ST_DEFER_R0_CACHED // shape probes (tools/defer_shape_probe.sh)
-#define ST_DEFER_R0_CACHED 2
+#define ST_DEFER_R0_CACHED 1
 #endif
 #ifndef ST_DEFER_PT0_CACHED
-#define ST_DEFER_PT0_CACHED 0u
+#define ST_DEFER_PT0_CACHED 4u
 #endif
-  constexpr int kR0 = NT ? 2 : ST_DEFER_R0_CACHED;
-  constexpr uint32_t kTile0 = NT ? 8u : ST_DEFER_PT0_CACHED;
+  // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
+  // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
+  // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
+  // row-major (1 row: 18 % slower at 8192^2 fp32,
+  // profiles/r02_flat_map_r1_f32_cached.log)
+  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  constexpr int kR0 = NT ? 2 : kF64C ? ST_DEFER_R0_CACHED : 2;
+  constexpr uint32_t kTile0 = NT ? 8u : kF64C ? ST_DEFER_PT0_CACHED : 0u;
   constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
   // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
   // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
