@@ -275,6 +275,7 @@ class ShardedSimilarityTransform:
         self._streams = (self.ops.make_streams()
                          if overlap and hasattr(self.ops, "make_streams") else None)
         self.mat = None
+        self._own_mat = False
         self.k = 0
         self.cur = 0
         # the per-round exchange: RCCL owned by the library ("native", the
@@ -331,12 +332,12 @@ class ShardedSimilarityTransform:
         p = self.part
         if mat is not None:
             assert tuple(mat.shape) == (p.nrows, p.n)
-            self.mat = mat
-        elif self.mat is not None and hasattr(self.ops, "generate_into") \
-                and tuple(self.mat.shape) == (p.nrows, p.n) and self.mat.dtype == self.dtype:
+            self.mat, self._own_mat = mat, False      # the caller's: never overwritten
+        elif self.mat is not None and self._own_mat and hasattr(self.ops, "generate_into"):
             self.ops.generate_into(kind, p.n, p.row0, seed, self.mat)
         else:
             self.mat = self.ops.generate(kind, p.n, self.dtype, p.nrows, p.row0, seed)
+            self._own_mat = True
         return self.mat
 
     def gather(self, s):

@@ -422,3 +422,23 @@ def test_rank_block_rehearsal_without_a_group(orc):
     for _ in range(2 * sd._defer_m):
         sd.deferred_round(0.0, 1000)
     assert ops.stores == 2
+
+
+class _IntoOps(CpuShardOps):
+    """CpuShardOps that can regenerate a block in place (as HipShardOps)."""
+
+    def generate_into(self, kind, n, row0, seed, out):
+        out.copy_(self.generate(kind, n, out.dtype, out.shape[0], row0, seed))
+
+
+def test_load_regenerates_only_its_own_block():
+    """load() regenerates a block it allocated itself in place (no second
+    multi-GiB allocation) but never writes into a caller's tensor."""
+    sh = ShardedSimilarityTransform(16, torch.float64, ops=_IntoOps())
+    a = sh.load("random", seed=1)
+    a.fill_(0.0)
+    assert sh.load("random", seed=1) is a and float(a.sum()) > 0     # regenerated in place
+    mine = torch.full((16, 16), 7.0, dtype=torch.float64)
+    assert sh.load(mat=mine) is mine
+    b = sh.load("random", seed=1)
+    assert b is not mine and bool((mine == 7.0).all())              # caller's tensor untouched
