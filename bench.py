@@ -753,28 +753,34 @@ def run_leg(name, a):
 LEG_TAG = "@@LEG "
 
 
+LEG_FAILURES = []
+
+
 def child_leg(name, a):
     """Run leg `name` in a fresh child process (`bench.py --leg`) and return
-    its result; if the child fails, run it in this process instead and say
-    so in the result (`in_process`)."""
+    its result, or None if the child failed or timed out.  A failed leg is
+    NOT re-run here (this process holds the GPU and the headline's
+    allocations, the condition the child process exists to avoid, and a
+    leg that faulted or hung must not be repeated): the failure goes into
+    the line's `leg_failures` and the leg's keys are left out."""
     import torch
-    torch.cuda.synchronize()
-    torch.cuda.empty_cache()
+    if torch.cuda.is_initialized():
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     env = {k: v for k, v in os.environ.items()
            if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
     cmd = [sys.executable, os.path.abspath(__file__), "--leg", name, "--leg-args", json.dumps(a)]
-    err = None
     try:
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         for ln in reversed(r.stdout.splitlines()):
             if ln.startswith(LEG_TAG):
                 return json.loads(ln[len(LEG_TAG):])
         err = f"child exited {r.returncode}: {r.stderr[-400:]}"
-    except Exception as e:  # noqa: BLE001 - fall back below
+    except Exception as e:  # noqa: BLE001 - reported in the line
         err = repr(e)[:400]
-    res = run_leg(name, a)
-    res["in_process"] = err
-    return res
+    LEG_FAILURES.append({"leg": name, "error": err})
+    print(f"bench.py: leg {name} failed: {err}", file=sys.stderr, flush=True)
+    return None
 
 
 def leg_main(args):
@@ -944,10 +950,11 @@ def main():
     # headline's launches only)
     weak_blocks = None
     if world == 1 and not args.strong and args.dtype == "f64":
-        weak_blocks = child_leg("weak_rank_blocks", {
+        wb = child_leg("weak_rank_blocks", {
             "device": dev_index, "steps": args.steps, "warmup": args.warmup,
             "kind": args.kind, "n": args.n, "dtype": args.dtype,
-            "representative": representative})["weak_rank_blocks"]
+            "representative": representative})
+        weak_blocks = None if wb is None else wb["weak_rank_blocks"]
 
     out = {"metric": "ms/iteration + achieved HBM GB/s (% roofline), N×N Hilbert fp64",
            "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -980,31 +987,44 @@ def main():
     # streams 1-2.5 % slower - tools/alloc_probe.py --pre,
     # profiles/r02_alloc_probe_pre.log - so every full-size leg gets a
     # process of its own, the way the driver's fresh N = 1 run gets its
-    # headline block; a child that fails is re-run here in-process)
+    # headline block; a child that fails is reported in `leg_failures`, not
+    # re-run here)
     if world == 1 and full:
         sh_args = {"device": dev_index, "steps": args.steps, "warmup": args.warmup,
                    "kind": args.kind, "n": n, "dtype": args.dtype,
                    "representative": representative}
         ns = child_leg("north_star", sh_args)
-        out["north_star"] = ns["north_star"]
-        out["north_star"]["matrix_free"] = child_leg(
-            "north_star_mf", dict(sh_args, lam_ns=ns["north_star"]["eigen_val"]))["matrix_free"]
+        every_ms = {workload: el / args.steps * 1e3}
+        if ns is not None:
+            out["north_star"] = ns["north_star"]
+            every_ms["random32768_f64"] = ns["every_ms"]
+            mf = child_leg("north_star_mf",
+                           dict(sh_args, lam_ns=ns["north_star"]["eigen_val"]))
+            if mf is not None:
+                out["north_star"]["matrix_free"] = mf["matrix_free"]
         c4 = child_leg("configs4", sh_args)
-        out["configs4_f32"] = c4["configs4_f32"]
-        every_ms = {"random32768_f64": ns["every_ms"], "random32768_f32": c4["every_ms"],
-                    workload: el / args.steps * 1e3}
+        if c4 is not None:
+            out["configs4_f32"] = c4["configs4_f32"]
+            every_ms["random32768_f32"] = c4["every_ms"]
         deferred = {}
-        for i in range(3):
+        for i, key in enumerate((workload, "random32768_f64", "random32768_f32")):
+            if key not in every_ms:      # its every-round leg failed: no reference time
+                continue
             d = child_leg("deferred", dict(sh_args, which=i, every_ms=every_ms))
-            deferred.update(d["deferred_writes"])
+            if d is not None:
+                deferred.update(d["deferred_writes"])
         out["deferred_writes"] = deferred
-        if "configs[4] random32768_f32" in deferred:
+        if "configs[4] random32768_f32" in deferred and "configs4_f32" in out:
             out["configs4_f32"]["deferred_writes"] = deferred["configs[4] random32768_f32"]
         if not args.no_configs3:
-            c3 = child_leg("configs3", sh_args)["configs3_p1"]
-            c3["rank_blocks"] = child_leg("rank_blocks", sh_args)["rank_blocks"]
-            out["configs3_p1"] = c3
-            out["configs3_p1_ms_per_iteration"] = c3["ms_per_iteration"]
+            c3 = child_leg("configs3", sh_args)
+            if c3 is not None:
+                c3 = c3["configs3_p1"]
+                rb = child_leg("rank_blocks", sh_args)
+                if rb is not None:
+                    c3["rank_blocks"] = rb["rank_blocks"]
+                out["configs3_p1"] = c3
+                out["configs3_p1_ms_per_iteration"] = c3["ms_per_iteration"]
 
     # ---- N > 1: configs[3] strong-scaled over the world ------------------
     if world > 1 and not args.no_configs3:
@@ -1058,6 +1078,8 @@ def main():
         out["cpu_baseline"] = cb
         out["speedup_vs_cpu"] = round(per_round_ms / out["ms_per_step"], 1)
 
+    if LEG_FAILURES:
+        out["leg_failures"] = LEG_FAILURES
     if not representative:
         out = strip_fracs(out)
         out["representative"] = False

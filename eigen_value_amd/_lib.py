@@ -114,6 +114,7 @@ def _declare(L: ctypes.CDLL) -> None:
     L.eigen_last_error.argtypes = []
     L.eigen_last_error.restype = ctypes.c_char_p
     L.st_version.restype = ctypes.c_char_p
+    L.st_probe_switches.restype = ctypes.c_char_p
     L.st_device_count.restype = i32
     L.max_eigen_value.argtypes = [P, P, P, P, u32, P]
     L.max_eigen_value.restype = i64

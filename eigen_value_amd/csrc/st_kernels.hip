@@ -17,6 +17,39 @@
 #include "st_device.h"
 #include "st_internal.h"
 
+// A/B probe switches of the launch shapes (st_device.h has those of the
+// kernel code: ST_DPP_NOINIT, ST_ROW_VLOAD, ST_FLAT_UNMASKED,
+// ST_DEFER_STORE_NT).  Probe builds of the library
+// (tools/defer_shape_probe.sh) pass -DST_PROBES=1 with other values; a
+// library build with any other value fails here, and st_version() names the
+// switches a probe build was made with.
+#ifndef ST_EVERY_CACHED_R1 // 0 = round 2's 2 rows, row-major
+#define ST_EVERY_CACHED_R1 1
+#endif
+#ifndef ST_DEFER_R0_CACHED // rows of the cached fp64 NP = 0 round (1, 2, 4)
+#define ST_DEFER_R0_CACHED 1
+#endif
+#ifndef ST_DEFER_PT0_CACHED // its piece tile (0 = row-major)
+#define ST_DEFER_PT0_CACHED 4u
+#endif
+#ifndef ST_DEFER_STORE_R8_CACHED // 8 rows for the cached fp64 5-pending store
+#define ST_DEFER_STORE_R8_CACHED 1
+#endif
+#define ST_PROBES_DEFAULT                                                      \
+  (ST_DPP_NOINIT == 1 && ST_ROW_VLOAD == 0 && ST_FLAT_UNMASKED == 1 &&         \
+   ST_DEFER_STORE_NT == 0 && ST_EVERY_CACHED_R1 == 1 &&                        \
+   ST_DEFER_R0_CACHED == 1 && ST_DEFER_PT0_CACHED == 4 &&                      \
+   ST_DEFER_STORE_R8_CACHED == 1)
+#ifndef ST_PROBES
+static_assert(ST_PROBES_DEFAULT,
+              "A/B probe switch set in a library build (use -DST_PROBES=1)");
+#endif
+static_assert(ST_DEFER_R0_CACHED == 1 || ST_DEFER_R0_CACHED == 2 ||
+                ST_DEFER_R0_CACHED == 4,
+              "ST_DEFER_R0_CACHED: 1, 2 or 4 rows");
+#define ST_STR2(x) #x
+#define ST_STR(x) ST_STR2(x)
+
 namespace st {
 namespace {
 
@@ -198,9 +231,6 @@ constexpr int kFlatU =
 //                        vs 0.159, 2880 x 23040 0.155 vs 0.159
 //   cached fp32 blocks   2 rows, row-major (1 row or tiles lose 0-3 %)
 // Which rows a workgroup takes, and in what order, changes no result.
-#ifndef ST_EVERY_CACHED_R1 // A/B probe: 0 = round 2's 2 rows, row-major
-#define ST_EVERY_CACHED_R1 1
-#endif
 template <typename T, bool NT>
 constexpr int kFlatEveryRows =
   (sizeof(T) == 8 && !NT && ST_EVERY_CACHED_R1) ? 1 : kFlatRows;
@@ -706,12 +736,6 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV>(                           \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, store, flush, PTV, stream)
-#ifndef ST_DEFER_R0_CACHED // shape probes (tools/defer_shape_probe.sh)
-#define ST_DEFER_R0_CACHED 1
-#endif
-#ifndef ST_DEFER_PT0_CACHED
-#define ST_DEFER_PT0_CACHED 4u
-#endif
   // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
   // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
   // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
@@ -723,9 +747,6 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
   // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
   // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
-#ifndef ST_DEFER_STORE_R8_CACHED // A/B probe switch
-#define ST_DEFER_STORE_R8_CACHED 1
-#endif
   // cached fp64 blocks: 8 rows tiled by 4 for the storing round with 5
   // pending (8192^2 0.160 vs 0.165 ms, the P = 8 block level;
   // profiles/r02_flat_map_r8_f64_cached_store5.log)
@@ -771,6 +792,13 @@ launch_round_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   ST_REQUIRE(flush || (s_next && inv_next), "round_flat_deferred: null pointer");
   ST_REQUIRE(npend < defer_rounds(nrows, ncols, sizeof(T)),
              "round_flat_deferred: %u pending rounds", npend);
+  // the m-th round of a group (m - 1 pending) is the storing one: a round
+  // that does not store re-applies at most m - 2 (launch_flat_deferred has
+  // no read-only kernel for m - 1)
+  ST_REQUIRE(store || npend + 1 < defer_rounds(nrows, ncols, sizeof(T)),
+             "round_flat_deferred: %u pending rounds without a store (the "
+             "round with %u pending stores)",
+             npend, defer_rounds(nrows, ncols, sizeof(T)) - 1);
   ST_REQUIRE(!flush || store, "round_flat_deferred: a flush stores");
   ST_REQUIRE(ncols > 0 && nrows > 0 && row0 + (uint64_t)nrows <= ncols,
              "round_flat_deferred: bad block");
@@ -1334,6 +1362,21 @@ ST_STEP_EXPORTS(double, f64)
 
 ST_DEFER_EXPORTS(float, f32)
 ST_DEFER_EXPORTS(double, f64)
+
+const char*
+st_probe_switches(void)
+{
+  return ST_PROBES_DEFAULT
+           ? "defaults"
+           : "ST_DPP_NOINIT=" ST_STR(ST_DPP_NOINIT) " ST_ROW_VLOAD=" ST_STR(
+               ST_ROW_VLOAD) " ST_FLAT_UNMASKED=" ST_STR(ST_FLAT_UNMASKED)
+               " ST_DEFER_STORE_NT=" ST_STR(ST_DEFER_STORE_NT)
+                 " ST_EVERY_CACHED_R1=" ST_STR(ST_EVERY_CACHED_R1)
+                   " ST_DEFER_R0_CACHED=" ST_STR(ST_DEFER_R0_CACHED)
+                     " ST_DEFER_PT0_CACHED=" ST_STR(ST_DEFER_PT0_CACHED)
+                       " ST_DEFER_STORE_R8_CACHED=" ST_STR(
+                         ST_DEFER_STORE_R8_CACHED);
+}
 
 unsigned int
 st_defer_rounds(unsigned int nrows, unsigned int ncols, int dtype)

@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "st_internal.h"
@@ -450,7 +451,12 @@ eigen_last_error(void)
 const char*
 st_version(void)
 {
-  return "eigen_value_amd 0.1.0 (gfx950)";
+  // the A/B probe switches the kernels were built with (st_kernels.hip):
+  // "defaults" in every library build, the values in a probe build
+  static const std::string v =
+    std::string("eigen_value_amd 0.3.0 (gfx950; probe switches: ") +
+    st_probe_switches() + ")";
+  return v.c_str();
 }
 
 int

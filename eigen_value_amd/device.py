@@ -226,7 +226,10 @@ def flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next, part, v, state,
     matrix stored every round."""
     import ctypes
     _check_cuda(mat, s_cur, inv_cur, part, v, state, *pend_s, *pend_inv)
-    assert len(pend_s) == len(pend_inv) < defer_rounds(*mat.shape, mat.dtype)
+    m = defer_rounds(*mat.shape, mat.dtype)
+    assert len(pend_s) == len(pend_inv) < m
+    # the round with m - 1 pending is the group's storing round
+    assert store or len(pend_s) + 1 < m, "a round with m - 1 pending rounds must store"
     assert mat.is_contiguous() and mat.dim() == 2
     nrows, ncols = mat.shape
     assert s_cur.numel() >= ncols and inv_cur.numel() >= ncols and v.numel() >= ncols

@@ -328,7 +328,13 @@ class ShardedSimilarityTransform:
         is regenerated in place where the ops can (no second multi-GiB
         allocation: one made after others in a process streams 1-2.5 %
         slower, profiles/r02_alloc_probe_pre.log); the returned tensor is
-        then the same one."""
+        then the same one.
+
+        Aliasing: the tensor an earlier ``load()`` returned IS the block
+        this object works on, so rounds, solves and a later ``load()``
+        overwrite it (clone it to keep A_0).  A tensor passed as ``mat=`` is
+        the caller's: a later ``load()`` allocates a new block rather than
+        regenerating into it (but rounds still transform it in place)."""
         p = self.part
         if mat is not None:
             assert tuple(mat.shape) == (p.nrows, p.n)

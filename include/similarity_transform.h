@@ -340,9 +340,10 @@ unsigned int st_set_flat_grid_limit(unsigned int max_x);
  * = 1 / d_s_cur; d_inv_next receives 1 / s_{k+1} for the block's rows (pass
  * the rank's slot, like d_s_next).  flush = 1 (with store = 1) only stores
  * A_{k+1} - no row sums, no v update - to leave the matrix as storing every
- * round would after the last round k.  npend < st_defer_rounds(nrows,
- * ncols, dtype), the rounds per store.  d_pend_s / d_pend_inv are HOST arrays
- * of device pointers. */
+ * round would after the last round k.  npend < m = st_defer_rounds(nrows,
+ * ncols, dtype), the rounds per store, and a round with npend = m - 1 (the
+ * group's last) must store: other calls return -1.  d_pend_s / d_pend_inv
+ * are HOST arrays of device pointers. */
 int st_round_flat_deferred_f32(float* d_mat, const float* d_s_cur,
                                const float* d_inv_cur, float* d_s_next,
                                float* d_inv_next, float* d_part, float* d_v,
@@ -466,8 +467,11 @@ int st_epilogue_f64(const double* d_s, double* d_v, unsigned int n,
                     double eps, unsigned int max_itr, unsigned int semantics,
                     st_state* d_state, void* stream);
 
-/* Library / device facts. */
+/* Library / device facts.  st_version names the library, the target and
+ * the A/B probe switches its kernels were built with ("defaults" in every
+ * library build; st_probe_switches returns that part alone). */
 const char* st_version(void);
+const char* st_probe_switches(void);
 int st_device_count(void);
 
 #ifdef __cplusplus

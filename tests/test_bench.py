@@ -125,3 +125,56 @@ def test_bench_leg_child_mode():
     leg = json.loads(tagged[0][len(bench.LEG_TAG):])["deferred_writes"]["configs[1] hilbert8192_f64"]
     assert leg["bitwise_equal_to_write_every_round"] is True and leg["stores_every"] == 6
     assert 0 < leg["ms_per_iteration"] < 0.157
+
+
+def test_failed_leg_is_reported_not_rerun(monkeypatch):
+    """A full-size leg whose child process fails is reported in
+    `leg_failures` and left out; it is never re-run in the parent (which
+    holds the GPU and the headline's allocations)."""
+    ran = []
+    monkeypatch.setattr(bench, "run_leg", lambda *a, **k: ran.append(a) or {"x": 1})
+    monkeypatch.setattr(bench, "LEG_FAILURES", [])
+
+    class R:
+        returncode, stdout, stderr = 134, "noise\n", "Aborted (core dumped)"
+    monkeypatch.setattr(bench.subprocess, "run", lambda *a, **k: R())
+    assert bench.child_leg("north_star", {"device": 0}) is None
+    assert not ran
+    assert bench.LEG_FAILURES == [{"leg": "north_star",
+                                   "error": "child exited 134: Aborted (core dumped)"}]
+
+    def hang(*a, **k):
+        raise bench.subprocess.TimeoutExpired("bench.py", 900)
+    monkeypatch.setattr(bench.subprocess, "run", hang)
+    assert bench.child_leg("configs3", {"device": 0}) is None
+    assert not ran and bench.LEG_FAILURES[-1]["leg"] == "configs3"
+    assert "TimeoutExpired" in bench.LEG_FAILURES[-1]["error"]
+
+
+@pytest.mark.gpu
+def test_bench_self_spawned_eight_ranks_on_one_gpu():
+    """The driver's 8-GPU partition, rehearsed on one GPU: `bench.py --gpus 8
+    --one-gpu --backend gloo` self-spawns 8 ranks on cuda:0 (gloo exchange).
+    The weak-scaled headline runs 23040^2 in blocks of 2880 rows and
+    configs[3] (65536^2 fp64) in blocks of 8192 rows per rank - spawn, port,
+    per-round gather, deferred-write ring, flush and teardown at world 8 -
+    and the configs[3] solve matches the oracle's P = 1 solve."""
+    out = subprocess.run(
+        [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "8", "--one-gpu",
+         "--backend", "gloo", "--steps", "5", "--warmup", "1", "--no-overlap-leg"],
+        capture_output=True, text=True, timeout=600, cwd=REPO,
+        env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert out.returncode == 0, out.stderr[-4000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 8 and d["representative"] is False
+    assert d["config"]["n"] == 23040 and d["config"]["rows_per_gpu"] == 2880
+    assert "frac" not in d["roofline"]
+    c3 = d["configs3_strong"]
+    assert c3["n"] == 65536 and c3["rows_per_gpu"] == 8192 and c3["n_gpus"] == 8
+    assert c3["solve"]["check"]["iter_count_equal"] is True
+    assert c3["solve"]["check"]["eigen_val_rel_err_vs_oracle"] <= 1e-10
+    assert c3["solve"]["check"]["eigen_val_rel_err_vs_true"] <= 1e-6
+    assert "deferred_writes" in c3 and c3["deferred_writes"]["stores_every"] == 6
+    assert d["exchange"]["backend"] == "gloo" and d["rccl_ranks"] is None

@@ -136,3 +136,27 @@ def test_launch_policy_queries():
     assert L.st_defer_rounds(8192, 8192, 0) == 6
     assert L.st_defer_rounds(32768, 32768, 1) == 6
     assert L.st_defer_rounds(16384, 16384, 1) == 6         # 2 GiB: non-temporal
+
+
+def test_probe_switches_are_the_shipped_defaults():
+    """A library build carries no A/B probe switch (st_kernels.hip fails to
+    compile with one unless -DST_PROBES=1), and st_version says so."""
+    L = _lib.load()
+    assert L.st_probe_switches() == b"defaults"
+    assert b"probe switches: defaults" in L.st_version()
+
+
+def test_deferred_round_without_store_is_rejected_at_m_minus_1():
+    """st_round_flat_deferred: the round with m - 1 pending rounds is the
+    group's storing round; asked not to store it returns -1 with a message
+    (before this check it silently launched the 4-pending kernel and dropped
+    the 5th scaling).  Rejected on the host before any device call."""
+    L = _lib.load()
+    m = L.st_defer_rounds(8192, 8192, 1)
+    dummy = ctypes.c_void_p(4096)                 # never dereferenced: rejected first
+    arr = (ctypes.c_void_p * m)(*([4096] * m))
+    for fn in (L.st_round_flat_deferred_f64, L.st_round_flat_deferred_f32):
+        rc = fn(dummy, dummy, dummy, dummy, dummy, dummy, dummy, 8192, 8192, 0, 1e-3, 0, 1000, 0, arr, arr, m - 1, 0, 0, dummy, None)
+        assert rc < 0 and "without a store" in _lib.last_error()
+        rc = fn(dummy, dummy, dummy, dummy, dummy, dummy, dummy, 8192, 8192, 0, 1e-3, 0, 1000, 0, arr, arr, m, 1, 0, dummy, None)
+        assert rc < 0 and "pending rounds" in _lib.last_error()

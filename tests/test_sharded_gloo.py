@@ -442,3 +442,104 @@ def test_load_regenerates_only_its_own_block():
     assert sh.load(mat=mine) is mine
     b = sh.load("random", seed=1)
     assert b is not mine and bool((mine == 7.0).all())              # caller's tensor untouched
+
+
+# ---------------------------------------------------------------------------
+# world 8: the partition the driver's 8-GPU run uses (bench.py --gpus 8):
+# chunk = ceil(n / 8) rows per rank, the last block shorter
+# ---------------------------------------------------------------------------
+N8 = 8 * 13 - 5          # chunk 13: ranks 0..6 own 13 rows, rank 7 owns 8
+
+
+def _rank8_policy(rank):
+    """Deferral by RANK (not only by block size): ranks 3 and 7 (the short
+    last block) store every round, the others defer with m = 2, 3 or 4 by
+    rank - so one solve mixes deferring and plain ranks and three different
+    rounds-per-store."""
+    return (lambda nr: rank not in (3, 7)), (lambda nr: 2 + rank % 3)
+
+
+# (tag, kind, dtype, semantics, mode, max_itr, eps); mode: plain | defer |
+# mfree | overlap
+W8_CASES = [
+    ("plain_random_sycl", "random", torch.float64, _lib.ST_SEM_SYCL, "plain", 1000, 1e-3),
+    ("plain_hilbert_f32", "hilbert", torch.float32, _lib.ST_SEM_SYCL, "plain", 1000, 1e-3),
+    ("defer_random_sycl", "random", torch.float64, _lib.ST_SEM_SYCL, "defer", 1000, 1e-3),
+    ("defer_hilbert_mainpy", "hilbert", torch.float64, _lib.ST_SEM_MAINPY, "defer", 1000, 1e-3),
+    ("defer_fixed7", "random", torch.float64, _lib.ST_SEM_SYCL, "defer", 7, 0.0),
+    ("defer_fixed12", "random", torch.float64, _lib.ST_SEM_SYCL, "defer", 12, 0.0),
+    ("defer_fixed13", "hilbert", torch.float64, _lib.ST_SEM_SYCL, "defer", 13, 0.0),
+    ("mfree_random", "random", torch.float64, _lib.ST_SEM_SYCL, "mfree", 1000, 1e-3),
+    ("overlap_random", "random", torch.float64, _lib.ST_SEM_SYCL, "overlap", 1000, 1e-3),
+    ("overlap_hilbert_mainpy", "hilbert", torch.float64, _lib.ST_SEM_MAINPY, "overlap", 1000,
+     1e-3),
+]
+
+
+def _worker8(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        for tag, kind, dtype, semantics, mode, max_itr, eps in W8_CASES:
+            ops = CpuDeferOps(*_rank8_policy(rank)) if mode == "defer" else CpuShardOps()
+            sh = ShardedSimilarityTransform(N8, dtype, ops=ops, semantics=semantics,
+                                            matrix_free=mode == "mfree",
+                                            overlap=mode == "overlap")
+            sh.load(kind, seed=3)
+            lam, v, iters, rounds = sh.solve(eps=eps, max_itr=max_itr, batch=3)
+            np.savez(os.path.join(outdir, f"{tag}_{rank}.npz"), v=v.numpy(), a=sh.mat.numpy(),
+                     meta=np.array([lam, iters, rounds, sh.part.row0, sh.part.nrows,
+                                    sh.part.chunk, int(sh.deferred_writes),
+                                    getattr(ops, "stores", -1),
+                                    getattr(sh, "_defer_m", 0)], dtype=np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def world8_runs(tmp_path_factory):
+    out = tmp_path_factory.mktemp("world8")
+    mp.spawn(_worker8, args=(8, _free_port(), str(out)), nprocs=8, join=True)
+    return out
+
+
+@pytest.mark.parametrize("case", W8_CASES, ids=[c[0] for c in W8_CASES])
+def test_world8_sharded_solve_vs_oracle(world8_runs, orc, case):
+    """gloo world 8 over n = 8*13 - 5 = 99 (uneven last block of 8 rows):
+    the plain and the deferred-write solves are BIT-identical to the
+    oracle's single-process loop on every rank (λ, v, iteration count and
+    each rank's final row block; deferral mixed by rank, m = 2 / 3 / 4,
+    fixed round counts ending mid-group); the matrix-free and overlapped
+    forms agree to fp64 rounding and hold identical v on every rank."""
+    tag, kind, dtype, semantics, mode, max_itr, eps = case
+    npdt = np.float64 if dtype == torch.float64 else np.float32
+    mat = orc.hilbert(N8, npdt) if kind == "hilbert" else orc.random_matrix(N8, 3, npdt)
+    ref = orc.similarity_transform(mat, semantics, eps=npdt(eps), max_itr=max_itr)
+    a_end = None if mode in ("mfree", "overlap") else _oracle_final_matrix(
+        orc, mat, semantics, ref.rounds_evaluated)
+    v0 = None
+    kinds = set()
+    for r in range(8):
+        d = np.load(world8_runs / f"{tag}_{r}.npz")
+        lam, iters, rounds, row0, nrows, chunk, deferred, stores, m = d["meta"]
+        row0, nrows = int(row0), int(nrows)
+        assert int(chunk) == 13 and nrows == (8 if r == 7 else 13) and row0 == 13 * r
+        assert int(iters) == ref.iter_count and int(rounds) == ref.rounds_evaluated
+        v = d["v"]
+        v0 = v if v0 is None else v0
+        assert np.array_equal(v, v0)                       # identical on every rank
+        if mode in ("plain", "defer"):
+            assert npdt(lam) == ref.eigen_val
+            assert np.array_equal(v, ref.eigen_vec)
+            assert np.array_equal(d["a"], a_end[row0:row0 + nrows])
+        else:
+            assert abs(lam - ref.eigen_val) <= 1e-12 * ref.eigen_val
+            assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-12
+        if mode == "defer":
+            assert bool(deferred) == (r not in (3, 7))
+            if deferred:
+                assert int(m) == 2 + r % 3
+                assert int(stores) == -(-int(rounds) // int(m))   # + the flush
+            kinds.add((bool(deferred), int(m)))
+    if mode == "defer":
+        assert kinds == {(False, 0), (True, 2), (True, 3), (True, 4)}

@@ -9,7 +9,7 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 OBJ=$ROOT/build/variants/$NAME; OUT=$ROOT/eigen_value_amd/lib/variants/$NAME; mkdir -p $OBJ $OUT
 FL="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I$ROOT/include -I$ROOT/eigen_value_amd/csrc"
 for f in st_kernels st_solve st_multi; do
-  /opt/rocm/bin/hipcc $FL $DEFS -c $ROOT/eigen_value_amd/csrc/$f.hip -o $OBJ/$f.o &
+  /opt/rocm/bin/hipcc $FL -DST_PROBES=1 $DEFS -c $ROOT/eigen_value_amd/csrc/$f.hip -o $OBJ/$f.o &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $OUT/libsimilarity_transform.so $OBJ/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
