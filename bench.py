@@ -152,6 +152,16 @@ def spawn_ranks(n: int, argv) -> int:
     return (bad[0] if bad[0] > 0 else 1) if bad else 0
 
 
+_T0 = time.perf_counter()
+
+
+def progress(msg: str) -> None:
+    """One line on stderr per finished leg (rank 0 only): long multi-rank
+    runs show they are alive, and a log shows where a failed run stopped."""
+    if os.environ.get("RANK", "0") == "0":
+        print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
 def scaled_n(n1: int, world: int) -> int:
     if world == 1:
         return n1
@@ -411,6 +421,7 @@ def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representativ
     lam, v, it, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=1)
     torch.cuda.synchronize()
     solve_ms = (time.perf_counter() - t0) * 1e3
+    progress(f"configs[3] 65536^2 over {world}: solve {it} iterations ({solve_ms:.1f} ms)")
     pin, perron = oracle_pin("random65536_f64"), true_lambda(n, "f64", 0)
     check = {}
     if pin is not None:
@@ -774,6 +785,7 @@ def child_leg(name, a):
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900)
         for ln in reversed(r.stdout.splitlines()):
             if ln.startswith(LEG_TAG):
+                progress(f"leg {name} done")
                 return json.loads(ln[len(LEG_TAG):])
         err = f"child exited {r.returncode}: {r.stderr[-400:]}"
     except Exception as e:  # noqa: BLE001 - reported in the line
@@ -853,6 +865,7 @@ def main():
     lam, v, iters, rounds = sh.solve(eps=1e-3, max_itr=1000, batch=1)
     torch.cuda.synchronize()
     solve_ms = (time.perf_counter() - t0) * 1e3
+    progress(f"{workload}: solve {iters} iterations ({solve_ms:.1f} ms), world {world}")
     solve = {"eps": 1e-3, "iter_count": iters, "rounds_evaluated": rounds,
              "eigen_val": lam, "ms": round(solve_ms, 3)}
     if args.kind == "hilbert" and n == 8192 and args.dtype == "f64":
@@ -878,6 +891,7 @@ def main():
     bytes_round_local = 2.0 * p.nrows * n * b
     value = bytes_round_total * args.steps / el / 1e9
     achieved = rate(bytes_round_local, fused_ms)
+    progress(f"{workload}: {args.steps} timed rounds, {el / args.steps * 1e3:.4f} ms per round")
     flat_pays = dev.flat_round_pays(p.nrows, n, dt)
     flat = (not args.overlap) and flat_pays
     traffic = load_traffic(workload, "k_flat" if flat else "k_round")
@@ -924,6 +938,7 @@ def main():
                        "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
         ov.close()
         del ov
+        progress("overlapped-exchange leg done")
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
@@ -942,6 +957,7 @@ def main():
                    "eigen_val": lam_mf}
     mf.close()
     del mf
+    progress("matrix-free leg done")
 
     # ---- N = 1: the weak-scaled headline's per-GPU blocks at N = 2, 4, 8 --
     # (rank 0's block of n = 8192*sqrt(N), timed alone: the compute side of
@@ -1031,6 +1047,7 @@ def main():
         out["configs3_strong"] = configs3_leg(sharded, torch, dist, world, rank,
                                               max(5, min(args.steps, 20)),
                                               min(args.warmup, 3), representative)
+        progress(f"configs3_strong done: {out['configs3_strong']['ms_per_iteration']} ms per round")
 
     # ---- the reference's own headline, apples to apples ----------------
     # README.md:66-158 of the reference publishes whole solves of the fp32

@@ -59,6 +59,8 @@ for s in $STEPS; do
       step bench_overlap_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29514 bench.py --gpus 2 --steps 50 --warmup 5 --backend gloo --one-gpu --overlap --no-overlap-leg ;;
     spawn) # the N > 1 line without a launcher: two self-spawned ranks on one GPU (gloo)
       step bench_spawn_p2 900 python bench.py --gpus 2 --one-gpu --backend gloo --steps 20 --warmup 3 --no-overlap-leg ;;
+    spawn8) # the driver's 8-GPU partition rehearsed: 8 self-spawned ranks on one GPU (gloo)
+      step bench_spawn_p8 900 python bench.py --gpus 8 --one-gpu --backend gloo --steps 5 --warmup 1 ;;
     defer) # the deferred-write rounds over whole store cycles: rocprof + HIP events
       for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
         set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_${K}${N}_${DT}"; mkdir -p "$D"
