@@ -1,0 +1,366 @@
+// store_probe.hip — the deferred-write STORING round (k_flat with NP = m - 1
+// pending scalings, A stored) against alternative ways to feed it its row
+// scales, on non-temporal fp64 blocks.
+//
+// The shipped storing launch (k_flat<..., R = 8, NP = 5>, runtime
+// pend.store) re-applies 5 pending rounds and its own (12 fp64 multiplies per
+// element) and needs 6 x R row scales per workgroup (1/s of each round for
+// its R rows).  It loads them as scalar loads, one per row behind a
+// row-in-block branch: 48 conditional s_loads, each waited for alone
+// (scalar loads return out of order, a wave can only wait for all of them),
+// and their SGPRs spill into VGPR lanes.  The probe kernel k_sp takes the
+// same element math and partial sums (bitwise: checked against k_flat) with
+//   RS = 0  the row scales as unconditional scalar loads (adjacent rows
+//           merge into s_load_dwordx4 ... x16, one wait)
+//   RS = 1  the row scales staged through LDS: the first 6 R lanes of the
+//           workgroup load one each (vector loads, issued before the matrix
+//           loads so waiting for them does not wait for the matrix), one
+//           barrier, then every lane reads them as LDS broadcasts (VGPR
+//           operands: no SGPR pressure, no scalar waits)
+// by rows per workgroup R and piece tile PT (FlatPending::pt's order).
+//
+// Build: make -C tools store_probe
+// Run:   ./tools/store_probe 32768 8192x65536      (SP_CHECK=1: bitwise check)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "st_device.h"
+
+using namespace st::dev;
+
+#define HIPCHECK(x)                                                            \
+  do {                                                                         \
+    hipError_t e = (x);                                                        \
+    if (e != hipSuccess) {                                                     \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x,           \
+                   hipGetErrorString(e));                                      \
+      std::exit(2);                                                            \
+    }                                                                          \
+  } while (0)
+
+using T = double;
+using V = vec<double, 2>::type;
+constexpr int W = 2;
+constexpr int BLK = 256;
+constexpr int NW = BLK / 64;
+constexpr int kRing = 7;
+
+template <int NP>
+struct Pend
+{
+  const T* s[NP > 0 ? NP : 1];
+  const T* inv[NP > 0 ? NP : 1];
+};
+
+// workgroup b -> (row group, piece): row-major (pt = 0) or pt row groups of
+// one piece back to back (k_flat's piece-tiled order)
+__device__ __forceinline__ void
+sp_map(uint32_t b, uint32_t ppr, uint32_t ng, uint32_t pt, uint32_t& rg, uint32_t& p)
+{
+  if (pt != 0) {
+    const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
+    const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;
+    p = t / g;
+    rg = tile * pt + (t - p * g);
+  } else {
+    rg = b / ppr;
+    p = b - rg * ppr;
+  }
+}
+
+// full blocks only (nrows % R == 0, ncols % 512 == 0): the probe compares the
+// row-scale feeds, not the ragged edges
+template <int R, int NP, int RS, bool STORE>
+__global__ __launch_bounds__(BLK) void
+k_sp(T* a, const T* __restrict__ s_cur, const T* __restrict__ inv_cur, T* __restrict__ part,
+     uint32_t nrows, uint32_t ncols, uint32_t ppr, uint32_t pt, const st_state* state,
+     uint32_t k, Pend<NP> pend)
+{
+  if (flat_gated<kGatePlain>(state, k))
+    return;
+  constexpr int NS = NP + 1; // row-scale vectors: the pending rounds', then s_k's
+  __shared__ T rsh[RS == 1 ? NS : 1][R];
+  __shared__ T red[NW][R];
+  uint32_t rg, p;
+  sp_map(blockIdx.x, ppr, nrows / R, pt, rg, p);
+  const uint32_t r0 = rg * R;
+  if constexpr (RS == 1) {
+    // first: the row scales (before the matrix loads, so that waiting for
+    // them waits for nothing else)
+    if (threadIdx.x < NS * R) {
+      const uint32_t i = threadIdx.x / R, j = threadIdx.x - i * R;
+      const T* src = i < (uint32_t)NP ? pend.inv[i < NP ? i : 0] : inv_cur;
+      rsh[i][j] = src[r0 + j];
+    }
+  }
+  const uint32_t c0 = (p * BLK + threadIdx.x) * W;
+  const T* arow = a + (size_t)r0 * ncols + c0;
+  V x[R];
+#pragma unroll
+  for (int j = 0; j < R; j++)
+    x[j] = __builtin_nontemporal_load(reinterpret_cast<const V*>(arow + (size_t)j * ncols));
+  const V sc = *reinterpret_cast<const V*>(s_cur + c0);
+  V spc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+    spc[i] = *reinterpret_cast<const V*>(pend.s[i] + c0);
+  T sr[RS == 0 ? NS : 1][R];
+  if constexpr (RS == 0) {
+#pragma unroll
+    for (int i = 0; i < NS; i++) {
+      const T* src = i < NP ? pend.inv[i < NP ? i : 0] : inv_cur;
+#pragma unroll
+      for (int j = 0; j < R; j++)
+        sr[i][j] = src[r0 + j];
+    }
+  } else {
+    __syncthreads();
+  }
+  T acc[R];
+#pragma unroll
+  for (int i = 0; i < NP; i++) {
+#pragma unroll
+    for (int j = 0; j < R; j++) {
+      const T inv = RS == 0 ? sr[i][j] : rsh[i][j];
+      x[j] = x[j] * (inv * spc[i]);
+    }
+  }
+  T* wrow = a + (size_t)r0 * ncols + c0;
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    const T inv = RS == 0 ? sr[NP][j] : rsh[NP][j];
+    const V y = x[j] * (inv * sc); // cpp:324-325
+    if constexpr (STORE)
+      __builtin_nontemporal_store(y, reinterpret_cast<V*>(wrow + (size_t)j * ncols));
+    acc[j] = hsum<T, W>(y);
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j + 1 < R; j += 2) {
+    const T t = wave_sum_pair(acc[j], acc[j + 1]);
+    if (lane >= 62)
+      red[wave][j + (lane - 62)] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    T t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; w++)
+      t += red[w][threadIdx.x];
+    part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+  }
+}
+
+template <typename F>
+static float
+time_seq(F launch, int seq = 8, int reps = 7)
+{
+  hipEvent_t a, b;
+  HIPCHECK(hipEventCreate(&a));
+  HIPCHECK(hipEventCreate(&b));
+  for (int k = 0; k < seq; k++)
+    launch(k);
+  HIPCHECK(hipDeviceSynchronize());
+  std::vector<float> t;
+  for (int r = 0; r < reps; r++) {
+    HIPCHECK(hipEventRecord(a));
+    for (int k = 0; k < seq; k++)
+      launch(k);
+    HIPCHECK(hipEventRecord(b));
+    HIPCHECK(hipEventSynchronize(b));
+    float ms;
+    HIPCHECK(hipEventElapsedTime(&ms, a, b));
+    t.push_back(ms / seq);
+  }
+  HIPCHECK(hipEventDestroy(a));
+  HIPCHECK(hipEventDestroy(b));
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+struct Block
+{
+  unsigned nr, n, ppr;
+  T* a;
+  T* s[kRing];
+  T* inv[kRing];
+  T* part;
+  T* v;
+  st_state* st;
+};
+
+static void
+report(const Block& b, const char* what, float ms, bool store)
+{
+  const double bytes = (store ? 2.0 : 1.0) * b.nr * (double)b.n * sizeof(T);
+  std::printf("  %-34s %8.4f ms  %7.1f GB/s\n", what, ms, bytes / (ms * 1e-3) / 1e9);
+  std::fflush(stdout);
+}
+
+// the library's launch: k_flat non-temporal fp64, FS stats, ALT, NP pending
+template <int R, int NP>
+static void
+lib_launch(const Block& b, int k, unsigned pt, bool store)
+{
+  constexpr int NPK = NP < 0 ? -1 : NP;
+  FlatPending<T, NPK> pd{};
+  for (int i = 0; i < (NP > 0 ? NP : 0); i++) {
+    pd.s[i] = b.s[1 + i];
+    pd.inv[i] = b.inv[1 + i];
+  }
+  pd.inv_cur = b.inv[0];
+  pd.store = store ? 1u : 0u;
+  pd.pt = pt;
+  const unsigned grid = b.nr / R * b.ppr;
+  hipLaunchKernelGGL((k_flat<T, W, 0, true, R, false, true, 2, 256, 0, kGatePlain, NPK, 1>),
+                     dim3(grid), dim3(256), 0, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, b.ppr,
+                     0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
+}
+
+template <int R, int NP, int RS, bool STORE>
+static void
+sp_launch(const Block& b, int k, unsigned pt)
+{
+  Pend<NP> pd{};
+  for (int i = 0; i < NP; i++) {
+    pd.s[i] = b.s[1 + i];
+    pd.inv[i] = b.inv[1 + i];
+  }
+  const unsigned grid = b.nr / R * b.ppr;
+  hipLaunchKernelGGL((k_sp<R, NP, RS, STORE>), dim3(grid), dim3(BLK), 0, 0, b.a, b.s[0],
+                     b.inv[0], b.part, b.nr, b.n, b.ppr, pt, b.st, (uint32_t)k, pd);
+}
+
+template <int R, int NP, int RS>
+static void
+sp_time(const Block& b, unsigned pt)
+{
+  const float ms = time_seq([&](int k) { sp_launch<R, NP, RS, true>(b, k, pt); });
+  char w[64];
+  std::snprintf(w, sizeof w, "k_sp NP=%d R=%d RS=%s PT=%u", NP, R, RS ? "lds" : "sgpr", pt);
+  report(b, w, ms, true);
+}
+
+static std::vector<unsigned> g_pts = { 0, 4, 16 };
+
+static void
+run(unsigned nr, unsigned n, bool check)
+{
+  Block b{};
+  b.nr = nr;
+  b.n = n;
+  b.ppr = n / (256 * W);
+  const size_t bytes = (size_t)nr * n * sizeof(T);
+  HIPCHECK(hipMalloc(&b.a, bytes));
+  for (int i = 0; i < kRing; i++) {
+    HIPCHECK(hipMalloc(&b.s[i], sizeof(T) * n));
+    HIPCHECK(hipMalloc(&b.inv[i], sizeof(T) * n));
+  }
+  HIPCHECK(hipMalloc(&b.part, sizeof(T) * (size_t)nr * b.ppr));
+  HIPCHECK(hipMalloc(&b.v, sizeof(T) * n));
+  HIPCHECK(hipMalloc(&b.st, sizeof(st_state)));
+  HIPCHECK(hipMemset(b.st, 0, sizeof(st_state)));
+  hipLaunchKernelGGL((k_generate<T, kRandom>), dim3(4096), dim3(256), 0, 0, b.a, nr, n, 0u,
+                     (uint64_t)7);
+  // distinct scale vectors (ring slot i: s = n/2 * (1 + (i+1) * c / n / 64))
+  for (int i = 0; i < kRing; i++) {
+    std::vector<T> h(n);
+    for (unsigned c = 0; c < n; c++)
+      h[c] = (T)(n / 2) * (1.0 + (i + 1) * (double)c / n / 64.0);
+    HIPCHECK(hipMemcpy(b.s[i], h.data(), sizeof(T) * n, hipMemcpyHostToDevice));
+    hipLaunchKernelGGL((k_recip<T>), dim3(64), dim3(256), 0, 0, b.s[i], b.inv[i], n);
+  }
+  HIPCHECK(hipDeviceSynchronize());
+  std::printf("%ux%u f64  %.3f GiB (non-temporal)\n", nr, n, bytes / double(1 << 30));
+  if (check) {
+    // one launch each from the same A: k_flat NP = 5 store vs k_sp RS = 0, 1
+    std::vector<T> a0(bytes / sizeof(T));
+    HIPCHECK(hipMemcpy(a0.data(), b.a, bytes, hipMemcpyDeviceToHost));
+    const size_t np = (size_t)nr * b.ppr;
+    std::vector<T> ra(a0.size()), rp(np), xa(a0.size()), xp(np);
+    lib_launch<8, 5>(b, 0, 0, true);
+    HIPCHECK(hipMemcpy(ra.data(), b.a, bytes, hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(rp.data(), b.part, np * sizeof(T), hipMemcpyDeviceToHost));
+    bool ok = true;
+    for (int rs = 0; rs < 2; rs++) {
+      HIPCHECK(hipMemcpy(b.a, a0.data(), bytes, hipMemcpyHostToDevice));
+      HIPCHECK(hipMemset(b.part, 0, np * sizeof(T)));
+      if (rs == 0)
+        sp_launch<8, 5, 0, true>(b, 0, 16);
+      else
+        sp_launch<8, 5, 1, true>(b, 0, 16);
+      HIPCHECK(hipMemcpy(xa.data(), b.a, bytes, hipMemcpyDeviceToHost));
+      HIPCHECK(hipMemcpy(xp.data(), b.part, np * sizeof(T), hipMemcpyDeviceToHost));
+      const bool same = std::memcmp(ra.data(), xa.data(), bytes) == 0 &&
+                        std::memcmp(rp.data(), xp.data(), np * sizeof(T)) == 0;
+      std::printf("  check k_sp RS=%d vs k_flat NP=5 store: %s\n", rs,
+                  same ? "bitwise equal" : "DIFFERENT");
+      ok = ok && same;
+    }
+    HIPCHECK(hipMemcpy(b.a, a0.data(), bytes, hipMemcpyHostToDevice));
+    if (!ok)
+      std::exit(3);
+  }
+  // references: the library's every-round launch (2 rows, tiles of 4) and
+  // its storing launch (8 rows, row-major, 5 pending)
+  report(b, "k_flat every-round R=2 PT=4",
+         time_seq([&](int k) { lib_launch<2, -1>(b, k, 4, true); }), true);
+  report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
+         time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
+  report(b, "k_flat store NP=0 R=8 PT=0",
+         time_seq([&](int k) { lib_launch<8, 0>(b, k, 0, true); }), true);
+  for (unsigned pt : g_pts) {
+    sp_time<8, 5, 0>(b, pt);
+    sp_time<8, 5, 1>(b, pt);
+    sp_time<4, 5, 0>(b, pt);
+    sp_time<4, 5, 1>(b, pt);
+    sp_time<2, 5, 1>(b, pt);
+    sp_time<8, 0, 1>(b, pt);
+  }
+  HIPCHECK(hipFree(b.a));
+  for (int i = 0; i < kRing; i++) {
+    HIPCHECK(hipFree(b.s[i]));
+    HIPCHECK(hipFree(b.inv[i]));
+  }
+  HIPCHECK(hipFree(b.part));
+  HIPCHECK(hipFree(b.v));
+  HIPCHECK(hipFree(b.st));
+}
+
+int
+main(int argc, char** argv)
+{
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: %s N|RxN ...\n", argv[0]);
+    return 1;
+  }
+  const bool check = std::getenv("SP_CHECK") != nullptr;
+  if (const char* e = std::getenv("SP_PT")) {
+    g_pts.clear();
+    for (const char* q = e; *q;) {
+      g_pts.push_back((unsigned)std::strtoul(q, nullptr, 10));
+      while (*q && *q != ',')
+        q++;
+      if (*q == ',')
+        q++;
+    }
+  }
+  for (int i = 1; i < argc; i++) {
+    unsigned nr = 0, n = 0;
+    if (std::sscanf(argv[i], "%ux%u", &nr, &n) != 2) {
+      n = (unsigned)std::atoi(argv[i]);
+      nr = n;
+    }
+    if (nr == 0 || n == 0 || nr > n || n % 512 || nr % 8) {
+      std::fprintf(stderr, "bad size %s (n %% 512 == 0, rows %% 8 == 0)\n", argv[i]);
+      return 1;
+    }
+    run(nr, n, check);
+  }
+  return 0;
+}
