@@ -958,6 +958,9 @@ struct FlatPending
   uint32_t store;   // store A_{k+1} this round
   uint32_t pt;      // piece-tiled workgroup order: pt row groups of a piece
                     // back to back (0 = row-major; see k_flat)
+  uint32_t pc;      // with pt: the pieces walked in column blocks of pc
+                    // pieces, each tiled as a block of its own (0 = one
+                    // column block; long rows, see k_flat)
 };
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
@@ -1037,11 +1040,21 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     // piece's column scales - s_k and the pending rounds' - in its L1
     // instead of refetching them from L2 (deferred rounds; and the
     // every-round launch on non-temporal blocks, tiles of 4)
+    // With pc (long rows): the pieces in column blocks of pc, the whole
+    // block's row groups tiled over one column block before the next
     const uint32_t pt = pend.pt, ng = (nrows + R - 1) / R;
-    const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
+    uint32_t bb = b, w = ppr, pb = 0;
+    if (pend.pc != 0 && pend.pc < ppr) { // uniform
+      const uint32_t cb = b / (ng * pend.pc);
+      pb = cb * pend.pc;
+      bb = b - cb * (ng * pend.pc);
+      w = ppr - pb < pend.pc ? ppr - pb : pend.pc;
+    }
+    const uint32_t tile = bb / (pt * w), t = bb - tile * (pt * w);
     const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;
     p = t / g;
     rg = tile * pt + (t - p * g);
+    p += pb;
   } else {
     rg = b / ppr;
     p = b - rg * ppr;

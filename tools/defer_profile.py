@@ -59,21 +59,39 @@ def np_of(name):
     return int(m.group(1).split(",")[11])
 
 
-def summarise(path, n, elem, m, workload, events=None):
+def summarise(path, n, elem, m, workload, events=None, launches=None):
+    """Per-NP averages of a kernel trace.  `launches`: also write the
+    deferred launches themselves (kernel, NP, start, duration; one row per
+    launch, in trace order) to this CSV - the trimmed trace that a committed
+    summary cites, so its averages can be re-derived from tracked files."""
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # noqa: E731
     flat, parts, last = {}, {}, None
+    kept = []
     for r in rows:
         name = r["Kernel_Name"]
         if "k_flat<" in name:
             last = np_of(name)
             flat.setdefault(last, []).append(dur(r))
+            kept.append(("k_flat", last, r))
         elif "k_parts<" in name and last is not None:
             parts.setdefault(last, []).append(dur(r))
+            kept.append(("k_parts", last, r))
             last = None
+    if launches:
+        t0 = int(kept[0][2]["Start_Timestamp"]) if kept else 0
+        with open(launches, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["kernel", "np", "start_ns", "duration_ns", "kernel_name"])
+            for kind, pos, r in kept:
+                w.writerow([kind, pos, int(r["Start_Timestamp"]) - t0,
+                            int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
+                            r["Kernel_Name"][:160]])
     nb = n * n * elem
     avg = lambda x: sum(x) / len(x)  # noqa: E731
-    out = {"workload": workload, "m": m, "trace": path, "k_flat": {}, "k_parts": {}}
+    out = {"workload": workload, "m": m,
+           "trace": os.path.basename(launches) if launches else path,
+           "k_flat": {}, "k_parts": {}}
     for pos in sorted(flat):
         t = avg(flat[pos])
         b = 2 * nb if pos in (-1, m - 1) else nb
@@ -139,6 +157,8 @@ if __name__ == "__main__":
                                     "mode: read it")
     p.add_argument("--trace", help="summarise a rocprofv3 kernel trace instead of running")
     p.add_argument("--json", help="summary mode: write the summary here")
+    p.add_argument("--launches", help="summary mode: write the per-launch rows (trimmed "
+                                      "trace) here; the summary cites this file")
     p.add_argument("--fetch", help="with --write: summarise FETCH_SIZE / WRITE_SIZE passes")
     p.add_argument("--write")
     a = p.parse_args()
@@ -148,7 +168,7 @@ if __name__ == "__main__":
     if a.trace or a.fetch:
         res = {}
         if a.trace:
-            res = summarise(a.trace, a.n, elem, m, wl, a.events)
+            res = summarise(a.trace, a.n, elem, m, wl, a.events, a.launches)
         if a.fetch and a.write:
             res["pmc"] = summarise_pmc(a.fetch, a.write, a.n, elem, m)
         if a.json:

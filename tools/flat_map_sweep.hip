@@ -46,6 +46,7 @@ constexpr int kSeq = 8;
 constexpr int kReps = 7;
 constexpr int kRing = 7; // s_k and up to 5 pending + 1
 static std::vector<unsigned> g_pts = { 0, 16 };
+static std::vector<unsigned> g_pcs = { 0 }; // FMS_PC: column blocks of pc pieces (0 = none)
 static int g_store_np = 3; // FMS_STORE_NP: the pending count of the storing round
 static int g_max_np = 3;   // FMS_MAX_NP (<= 5)
 static bool g_r8 = false;  // FMS_R8=1: 8 rows per workgroup instead of 2 and 4
@@ -93,7 +94,7 @@ struct Block
 
 template <typename T, bool NT, int R, int NP, int UF = 0>
 static void
-one(const Block<T>& b, unsigned pt)
+one(const Block<T>& b, unsigned pt, unsigned pc = 0)
 {
   constexpr int W = 16 / sizeof(T);
   // kFlatU (vector path), or UF chunks per piece
@@ -111,13 +112,15 @@ one(const Block<T>& b, unsigned pt)
     pd.inv_cur = b.inv[0];
     pd.store = store ? 1u : 0u;
     pd.pt = pt;
+    pd.pc = pc;
     hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NPK, U>),
                        dim3(grid), dim3(256), 0, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n,
                        ppr, 0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
   });
   const double bytes = (store ? 2.0 : 1.0) * b.nr * (double)b.n * sizeof(T);
-  std::printf("  NP=%2d R=%d PT=%5u nt=%d%s  %8.4f ms  %7.1f GB/s\n", NP, R, pt, (int)NT,
-              UF ? (UF == 1 ? " U=1" : UF == 2 ? " U=2" : " U=4") : "", ms, bytes / (ms * 1e-3) / 1e9);
+  std::printf("  NP=%2d R=%d PT=%5u PC=%4u nt=%d%s  %8.4f ms  %7.1f GB/s\n", NP, R, pt, pc,
+              (int)NT, UF ? (UF == 1 ? " U=1" : UF == 2 ? " U=2" : " U=4") : "", ms,
+              bytes / (ms * 1e-3) / 1e9);
   std::fflush(stdout);
 }
 
@@ -128,7 +131,9 @@ by_pt(const Block<T>& b)
 {
   for (unsigned pt : g_pts)
     if (NP >= 0 || pt == 0 || g_every)
-      one<T, NT, R, NP, UF>(b, pt);
+      for (unsigned pc : g_pcs)
+        if (pc == 0 || pt != 0)
+          one<T, NT, R, NP, UF>(b, pt, pc);
 }
 
 template <typename T, bool NT, int R>
@@ -259,16 +264,20 @@ main(int argc, char** argv)
   g_r8 = std::getenv("FMS_R8") != nullptr;
   g_r1 = std::getenv("FMS_R1") != nullptr;
   g_every = std::getenv("FMS_EVERY") != nullptr;
-  if (const char* e = std::getenv("FMS_PT")) { // e.g. FMS_PT=0,4,8,16,32
-    g_pts.clear();
+  auto parse_list = [](const char* e, std::vector<unsigned>& out) {
+    out.clear();
     for (const char* q = e; *q;) {
-      g_pts.push_back((unsigned)std::strtoul(q, nullptr, 10));
+      out.push_back((unsigned)std::strtoul(q, nullptr, 10));
       while (*q && *q != ',')
         q++;
       if (*q == ',')
         q++;
     }
-  }
+  };
+  if (const char* e = std::getenv("FMS_PT")) // e.g. FMS_PT=0,4,8,16,32
+    parse_list(e, g_pts);
+  if (const char* e = std::getenv("FMS_PC")) // e.g. FMS_PC=0,32,64
+    parse_list(e, g_pcs);
   for (int i = 2; i < argc; i++) {
     unsigned nr = 0, n = 0;
     if (std::sscanf(argv[i], "%ux%u", &nr, &n) != 2) {

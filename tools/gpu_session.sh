@@ -8,6 +8,7 @@ set -u
 TAG=${1:-run}; shift || true
 STEPS=${*:-tests smoke bench prof}
 OUT=gpurun_out/$TAG
+RTAG=${RTAG:-r03}   # round prefix of the files meant for profiles/
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 export HSA_ENABLE_IPC_MODE_LEGACY=0
@@ -61,14 +62,17 @@ for s in $STEPS; do
       step bench_spawn_p2 900 python bench.py --gpus 2 --one-gpu --backend gloo --steps 20 --warmup 3 --no-overlap-leg ;;
     spawn8) # the driver's 8-GPU partition rehearsed: 8 self-spawned ranks on one GPU (gloo)
       step bench_spawn_p8 900 python bench.py --gpus 8 --one-gpu --backend gloo --steps 5 --warmup 1 ;;
+    longrow) # configs[3]'s long-row rank blocks: column-block piece orders + the counter list
+      rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+      FMS_EVERY=1 FMS_PT=4 FMS_PC=0,16,32,64 step longrow_pc 600 ./tools/flat_map_sweep f64 32768 8192x65536 16384x65536 ;;
     defer) # the deferred-write rounds over whole store cycles: rocprof + HIP events
       for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
         set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_${K}${N}_${DT}"; mkdir -p "$D"
         step "defer_${K}${N}_${DT}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --events "$D/events.json"
-        python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --trace "$D/prof/run_kernel_trace.csv" --events "$D/events.json" --json "$D/cycle.json" | tee -a "$OUT/session.log"
+        python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --trace "$D/prof/run_kernel_trace.csv" --events "$D/events.json" --json "$D/${RTAG}_defer_cycle_${K}${N}_${DT}.json" --launches "$D/${RTAG}_defer_cycle_${K}${N}_${DT}_launches.csv" | tee -a "$OUT/session.log"
       done ;;
     defer_pmc) # HBM bytes per deferred launch (separate FETCH / WRITE passes)
-      for W in "random 32768 f64" "random 32768 f32"; do
+      for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
         set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_pmc_${K}${N}_${DT}"; mkdir -p "$D"
         step "defer_fetch_${K}${N}_${DT}" 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/fetch" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --cycles 3
         step "defer_write_${K}${N}_${DT}" 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/write" -o run -- python3 tools/defer_profile.py --kind $K --n $N --dtype $DT --cycles 3

@@ -75,7 +75,7 @@ sp_map(uint32_t b, uint32_t ppr, uint32_t ng, uint32_t pt, uint32_t& rg, uint32_
 
 // full blocks only (nrows % R == 0, ncols % 512 == 0): the probe compares the
 // row-scale feeds, not the ragged edges
-template <int R, int NP, int RS, bool STORE>
+template <int R, int NP, int RS, bool STORE, bool NTS = true>
 __global__ __launch_bounds__(BLK) void
 k_sp(T* a, const T* __restrict__ s_cur, const T* __restrict__ inv_cur, T* __restrict__ part,
      uint32_t nrows, uint32_t ncols, uint32_t ppr, uint32_t pt, const st_state* state,
@@ -135,8 +135,10 @@ k_sp(T* a, const T* __restrict__ s_cur, const T* __restrict__ inv_cur, T* __rest
   for (int j = 0; j < R; j++) {
     const T inv = RS == 0 ? sr[NP][j] : rsh[NP][j];
     const V y = x[j] * (inv * sc); // cpp:324-325
-    if constexpr (STORE)
+    if constexpr (STORE && NTS)
       __builtin_nontemporal_store(y, reinterpret_cast<V*>(wrow + (size_t)j * ncols));
+    else if constexpr (STORE)
+      *reinterpret_cast<V*>(wrow + (size_t)j * ncols) = y;
     acc[j] = hsum<T, W>(y);
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -202,12 +204,15 @@ report(const Block& b, const char* what, float ms, bool store)
   std::fflush(stdout);
 }
 
-// the library's launch: k_flat non-temporal fp64, FS stats, ALT, NP pending
-template <int R, int NP>
+// the library's launch: k_flat fp64 (non-temporal, 4 KB pieces, or cached,
+// 8 KB pieces), FS stats, ALT, NP pending; `lds` bytes of dynamic LDS per
+// workgroup cap the workgroups per CU
+template <int R, int NP, bool NT = true>
 static void
-lib_launch(const Block& b, int k, unsigned pt, bool store)
+lib_launch(const Block& b, int k, unsigned pt, bool store, unsigned lds = 0)
 {
   constexpr int NPK = NP < 0 ? -1 : NP;
+  constexpr int U = NT ? 1 : 2;
   FlatPending<T, NPK> pd{};
   for (int i = 0; i < (NP > 0 ? NP : 0); i++) {
     pd.s[i] = b.s[1 + i];
@@ -216,13 +221,60 @@ lib_launch(const Block& b, int k, unsigned pt, bool store)
   pd.inv_cur = b.inv[0];
   pd.store = store ? 1u : 0u;
   pd.pt = pt;
-  const unsigned grid = b.nr / R * b.ppr;
-  hipLaunchKernelGGL((k_flat<T, W, 0, true, R, false, true, 2, 256, 0, kGatePlain, NPK, 1>),
-                     dim3(grid), dim3(256), 0, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, b.ppr,
+  const unsigned ppr = b.n / (256 * W * U);
+  const unsigned grid = b.nr / R * ppr;
+  hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NPK, U>),
+                     dim3(grid), dim3(256), lds, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, ppr,
                      0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
 }
 
-template <int R, int NP, int RS, bool STORE>
+// dynamic LDS that leaves room for `c` workgroups per CU (160 KB of LDS per
+// CU; 0 = no cap)
+static unsigned
+lds_for(unsigned c)
+{
+  return c == 0 ? 0u : 163840u / c - 2048u;
+}
+
+// the shipped launch shapes of one store cycle (launch_flat_deferred) and
+// the every-round launch, each under workgroup-per-CU caps
+template <bool NT>
+static void
+cap_sweep(const Block& b)
+{
+  const unsigned caps[] = { 0, 8, 6, 5, 4, 3, 2 };
+  auto one = [&](const char* what, auto launch, bool store) {
+    for (unsigned c : caps) {
+      const unsigned lds = lds_for(c);
+      const float ms = time_seq([&](int k) { launch(k, lds); });
+      char w[96];
+      std::snprintf(w, sizeof w, "%s cap=%u/CU", what, c);
+      report(b, w, ms, store);
+    }
+  };
+  if (NT) {
+    one("every R=2 PT=4", [&](int k, unsigned l) { lib_launch<2, -1, NT>(b, k, 4, true, l); }, true);
+    one("NP=0 R=2 PT=8", [&](int k, unsigned l) { lib_launch<2, 0, NT>(b, k, 8, false, l); }, false);
+    one("NP=1 R=4 PT=32", [&](int k, unsigned l) { lib_launch<4, 1, NT>(b, k, 32, false, l); }, false);
+    one("NP=2 R=8 PT=32", [&](int k, unsigned l) { lib_launch<8, 2, NT>(b, k, 32, false, l); }, false);
+    one("NP=3 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 3, NT>(b, k, 16, false, l); }, false);
+    one("NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, NT>(b, k, 16, false, l); }, false);
+    one("store NP=5 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 0, true, l); }, true);
+    one("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 4, true, l); }, true);
+    one("store NP=5 R=4 PT=0", [&](int k, unsigned l) { lib_launch<4, 5, NT>(b, k, 0, true, l); }, true);
+  } else {
+    // cached fp64 blocks (< 2 GiB): 8 KB pieces
+    one("every R=1 PT=8", [&](int k, unsigned l) { lib_launch<1, -1, NT>(b, k, 8, true, l); }, true);
+    one("NP=0 R=1 PT=4", [&](int k, unsigned l) { lib_launch<1, 0, NT>(b, k, 4, false, l); }, false);
+    one("NP=1 R=4 PT=16", [&](int k, unsigned l) { lib_launch<4, 1, NT>(b, k, 16, false, l); }, false);
+    one("NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, NT>(b, k, 16, false, l); }, false);
+    one("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 4, true, l); }, true);
+  }
+}
+
+static unsigned g_lds = 0; // SP_LDS: dynamic LDS bytes per workgroup (caps workgroups per CU)
+
+template <int R, int NP, int RS, bool STORE, bool NTS = true>
 static void
 sp_launch(const Block& b, int k, unsigned pt)
 {
@@ -232,17 +284,18 @@ sp_launch(const Block& b, int k, unsigned pt)
     pd.inv[i] = b.inv[1 + i];
   }
   const unsigned grid = b.nr / R * b.ppr;
-  hipLaunchKernelGGL((k_sp<R, NP, RS, STORE>), dim3(grid), dim3(BLK), 0, 0, b.a, b.s[0],
+  hipLaunchKernelGGL((k_sp<R, NP, RS, STORE, NTS>), dim3(grid), dim3(BLK), g_lds, 0, b.a, b.s[0],
                      b.inv[0], b.part, b.nr, b.n, b.ppr, pt, b.st, (uint32_t)k, pd);
 }
 
-template <int R, int NP, int RS>
+template <int R, int NP, int RS, bool NTS = true>
 static void
 sp_time(const Block& b, unsigned pt)
 {
-  const float ms = time_seq([&](int k) { sp_launch<R, NP, RS, true>(b, k, pt); });
-  char w[64];
-  std::snprintf(w, sizeof w, "k_sp NP=%d R=%d RS=%s PT=%u", NP, R, RS ? "lds" : "sgpr", pt);
+  const float ms = time_seq([&](int k) { sp_launch<R, NP, RS, true, NTS>(b, k, pt); });
+  char w[96];
+  std::snprintf(w, sizeof w, "k_sp NP=%d R=%d RS=%s PT=%u%s LDS=%u", NP, R, RS ? "lds" : "sgpr",
+                pt, NTS ? "" : " cached-st", g_lds);
   report(b, w, ms, true);
 }
 
@@ -276,7 +329,8 @@ run(unsigned nr, unsigned n, bool check)
     hipLaunchKernelGGL((k_recip<T>), dim3(64), dim3(256), 0, 0, b.s[i], b.inv[i], n);
   }
   HIPCHECK(hipDeviceSynchronize());
-  std::printf("%ux%u f64  %.3f GiB (non-temporal)\n", nr, n, bytes / double(1 << 30));
+  std::printf("%ux%u f64  %.3f GiB (%s)\n", nr, n, bytes / double(1 << 30),
+              std::getenv("SP_CACHED") ? "cached launch shapes" : "non-temporal");
   if (check) {
     // one launch each from the same A: k_flat NP = 5 store vs k_sp RS = 0, 1
     std::vector<T> a0(bytes / sizeof(T));
@@ -308,19 +362,39 @@ run(unsigned nr, unsigned n, bool check)
   }
   // references: the library's every-round launch (2 rows, tiles of 4) and
   // its storing launch (8 rows, row-major, 5 pending)
-  report(b, "k_flat every-round R=2 PT=4",
-         time_seq([&](int k) { lib_launch<2, -1>(b, k, 4, true); }), true);
-  report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
-         time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
-  report(b, "k_flat store NP=0 R=8 PT=0",
-         time_seq([&](int k) { lib_launch<8, 0>(b, k, 0, true); }), true);
-  for (unsigned pt : g_pts) {
-    sp_time<8, 5, 0>(b, pt);
-    sp_time<8, 5, 1>(b, pt);
-    sp_time<4, 5, 0>(b, pt);
-    sp_time<4, 5, 1>(b, pt);
-    sp_time<2, 5, 1>(b, pt);
-    sp_time<8, 0, 1>(b, pt);
+  if (!std::getenv("SP_CAPS")) {
+    report(b, "k_flat every-round R=2 PT=4",
+           time_seq([&](int k) { lib_launch<2, -1>(b, k, 4, true); }), true);
+    report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
+           time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
+  }
+  if (std::getenv("SP_CAPS")) { // the library's shapes under workgroup-per-CU caps
+    if (std::getenv("SP_CACHED"))
+      cap_sweep<false>(b);
+    else
+      cap_sweep<true>(b);
+  } else if (std::getenv("SP_OCC")) { // workgroups per CU capped through dynamic LDS
+    for (unsigned lds : { 0u, 20480u, 32768u, 40960u, 54272u, 81920u }) {
+      g_lds = lds;
+      for (unsigned pt : g_pts) {
+        sp_time<8, 5, 0>(b, pt);
+        sp_time<8, 0, 1>(b, pt);
+        sp_time<2, 0, 1>(b, pt);
+        sp_time<4, 5, 0>(b, pt);
+      }
+    }
+    g_lds = 0;
+  } else {
+    for (unsigned pt : g_pts) {
+      sp_time<8, 5, 0>(b, pt);
+      sp_time<8, 5, 0, false>(b, pt);
+      sp_time<8, 5, 1>(b, pt);
+      sp_time<4, 5, 0>(b, pt);
+      sp_time<4, 5, 1>(b, pt);
+      sp_time<2, 5, 1>(b, pt);
+      sp_time<8, 0, 1>(b, pt);
+      sp_time<2, 0, 1>(b, pt);
+    }
   }
   HIPCHECK(hipFree(b.a));
   for (int i = 0; i < kRing; i++) {
