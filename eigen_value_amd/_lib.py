@@ -171,6 +171,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_defer_rounds.restype = u32
     L.st_set_flat_grid_limit.argtypes = [u32]
     L.st_set_flat_grid_limit.restype = u32
+    L.st_set_defer_caps.argtypes = [i32, i32, u32, u32]
+    L.st_set_defer_caps.restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32
     L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]

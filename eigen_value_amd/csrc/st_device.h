@@ -965,7 +965,8 @@ struct FlatPending
 
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false>
+          int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
+          int DS = -1>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -996,6 +997,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // columns after chunk u - 1 (the element-wide path, W = 1, takes U =
   // 16 / sizeof(T) so that its pieces hold as many bytes as the vector
   // path's)
+  // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
+  // compile time (1 / 0; the library's launches), or -1 = pend.store at
+  // run time (the sweep tools)
   if constexpr (GATE != kGateSpec) {
     if (flat_gated<GATE>(state, k))
       return;
@@ -1080,6 +1084,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // fp64; the every-round and NP = 0 forms lose up to 3 %,
   // profiles/r02_flat_map_ab_*.log)
   constexpr bool UM = SPLIT == 0 && NP > 0 && ST_FLAT_UNMASKED;
+  const bool do_store = NP < 0 || (DS >= 0 ? DS == 1 : pend.store != 0); // uniform
   // the deferred rounds' stores (probe switch ST_DEFER_STORE_NT: non-temporal
   // on cached blocks too)
   constexpr bool NTS = NT || (NP >= 0 && ST_DEFER_STORE_NT);
@@ -1087,14 +1092,18 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
   for (int u = 0; u < U; u++)
     cl[u] = (!UM || in_cols[u]) ? c0 + u * BLK * W : ncols - W;
+  // the group's rows walked from one base pointer by the row pitch (no
+  // per-row 64-bit multiply); rows past the block re-read its last row
+  const T* ap = a + (size_t)(r0 < nrows ? r0 : nrows - 1) * ncols;
 #pragma unroll
   for (int j = 0; j < R; j++) {
     acc[j] = (T)0;
     if constexpr (UM) {
-      const uint32_t rj = r0 + j < nrows ? r0 + j : nrows - 1; // uniform
 #pragma unroll
       for (int u = 0; u < U; u++)
-        x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)rj * ncols + cl[u]));
+        x[u][j] = ld<V, NT>(reinterpret_cast<const V*>(ap + cl[u]));
+      if (r0 + j + 1 < nrows) // uniform
+        ap += ncols;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++)
@@ -1132,7 +1141,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // NP = 4, 8 rows, tiles of 16: 1.23 vs 1.29 ms; the storing round with 5
   // pending and fp32 lose 1 - 2 %, their merged scales crowd the SGPRs)
   const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
-  constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && NP <= 4;
+  // (the storing round merges its row loads only with its store decision
+  // fixed at compile time, DS = 1: tools/store_probe, profiles/r03_store_probe*)
+  constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && (NP <= 4 || DS == 1);
   if (kMergeRows && r0 + R <= nrows) { // uniform
 #pragma unroll
     for (int j = 0; j < R; j++)
@@ -1203,6 +1214,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         }
       }
     }
+    T* wp = a + (size_t)r0 * ncols + c0 + u * BLK * W; // row r0 + j after j pitches
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
@@ -1211,8 +1223,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         y = x[u][j] * (inv * sc[u]); // cpp:324-325
       else
         y = (inv * x[u][j]) * sc[u]; // main.py:13-16
-      if ((NP < 0 || pend.store) && in_cols[u] && r0 + j < nrows)
-        st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W), y);
+      if (do_store && in_cols[u] && r0 + j < nrows)
+        st<V, NTS>(reinterpret_cast<V*>(wp), y);
+      wp += ncols;
       const T h = in_cols[u] ? hsum<T, W>(y) : (T)0;
       acc[j] = u == 0 ? h : acc[j] + h;
     }
@@ -1246,7 +1259,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
           y = x[u][j] * (inv * sc[u]); // cpp:324-325
         else
           y = (inv * x[u][j]) * sc[u]; // main.py:13-16
-        if (NP < 0 || pend.store)
+        if (do_store)
           st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
                     y);
         acc[j] = u == 0 ? hsum<T, W>(y) : acc[j] + hsum<T, W>(y);

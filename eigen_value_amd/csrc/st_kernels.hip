@@ -665,14 +665,14 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 8192^2 fp64 0.125 vs 0.158; fp32 (every 4th, 4 rows) 0.821 vs 1.350 and
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
-template <typename T, int W, int ORDER, bool NT, int NP, int R>
+template <typename T, int W, int ORDER, bool NT, int NP, int R, bool STORE>
 void
 launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         T* inv_next, T* part, T* v, uint32_t nrows,
                         uint32_t ncols, uint32_t row0, T eps, uint32_t k,
                         uint32_t max_itr, uint32_t semantics, st_state* st,
                         const T* const* pend_s, const T* const* pend_inv,
-                        bool store, bool flush, uint32_t pt, hipStream_t stream)
+                        bool flush, uint32_t pt, uint32_t lds, hipStream_t stream)
 {
   constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
@@ -684,18 +684,54 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
     pd.inv[i] = pend_inv[i];
   }
   pd.inv_cur = inv_cur;
-  pd.store = store ? 1u : 0u;
+  pd.store = STORE ? 1u : 0u;
   pd.pt = pt;
   const FlatGrid fg = flat_grid(grid);
+  // lds: dynamic LDS the kernel does not use, reserved only to cap the
+  // workgroups per CU (see launch_flat_deferred)
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
-                                  kBlock, 0, dev::kGatePlain, NP, U>),
-                     fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v,
+                                  kBlock, 0, dev::kGatePlain, NP, U, false,
+                                  STORE ? 1 : 0>),
+                     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
   if (!flush) // a flush only stores the matrix: s, v and the state stand
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
                        part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
                        0u, 0u, 0u, inv_next);
+}
+
+// Workgroups per CU of the deferred rounds' launches (0 = as many as the
+// registers allow).  A launch that keeps R = 4 or 8 rows x 16 B per lane in
+// flight oversubscribes the memory system at full occupancy (5-6
+// workgroups, up to 192 KB of loads per CU): capping it - with dynamic LDS
+// the kernel does not use, the only hard cap on workgroups per CU - is
+// faster (tools/store_probe SP_CAPS=1, profiles/r03_store_probe_caps_*.log:
+// the non-temporal storing round 2.85 -> 2.77 ms at 3 per CU, 32768^2
+// fp64).  Indexed [fp64][non-temporal][slot], slot = the pending count of a
+// read-only round (0 ... 4) or kCapStore for a storing one.
+constexpr int kCapStore = 6;
+std::atomic<uint32_t> g_defer_caps[2][2][7] = {
+  // fp32: cached, non-temporal
+  { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 0, 0, 0, 0, 0, 0 } },
+  // fp64: cached, non-temporal
+  { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 0, 0, 0, 0, 0, 0 } },
+};
+
+// dynamic LDS that leaves room for `cap` workgroups per CU (160 KB of LDS
+// per CU on gfx950, k_flat's own few hundred bytes included)
+inline uint32_t
+defer_cap_lds(uint32_t cap)
+{
+  return cap < 2 ? 0u : (160u << 10) / cap - 2048u;
+}
+
+template <typename T, bool NT>
+inline uint32_t
+defer_lds(uint32_t slot)
+{
+  return defer_cap_lds(
+    g_defer_caps[sizeof(T) == 8][NT][slot].load(std::memory_order_relaxed));
 }
 
 // Launch shape of the deferred rounds by pending count NP
@@ -732,10 +768,14 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
-#define ST_NP(NPV, RV, PTV)                                                    \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV>(                           \
+#define ST_NP(NPV, RV, PTV, LDS)                                               \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, false>(                    \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
-    max_itr, semantics, st, pend_s, pend_inv, store, flush, PTV, stream)
+    max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
+#define ST_NPS(NPV, RV, PTV, LDS)                                              \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, true>(                     \
+    a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
+    max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
   // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
   // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
   // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
@@ -757,24 +797,27 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr int kR2 = NT ? 8 : 4; // NP = 2: 1-2 % with 8 rows, non-temporal only
   static_assert(kDeferRoundsMax == 6, "one case per pending count below");
   if (store) {
+    const uint32_t lds = defer_lds<T, NT>(kCapStore);
     switch (npend) {
-    case 0: ST_NP(0, 4, 0u); break;
-    case 1: ST_NP(1, kRS, 0u); break;
-    case 2: ST_NP(2, kRS, 0u); break;
-    case 3: ST_NP(3, kRS, 0u); break;
-    case 4: ST_NP(4, kRS, 0u); break;
-    default: ST_NP(5, kRS5, kTileS5); break;
+    case 0: ST_NPS(0, 4, 0u, lds); break;
+    case 1: ST_NPS(1, kRS, 0u, lds); break;
+    case 2: ST_NPS(2, kRS, 0u, lds); break;
+    case 3: ST_NPS(3, kRS, 0u, lds); break;
+    case 4: ST_NPS(4, kRS, 0u, lds); break;
+    default: ST_NPS(5, kRS5, kTileS5, lds); break;
     }
   } else {
+    const uint32_t lds = defer_lds<T, NT>(npend < 5 ? npend : 4);
     switch (npend) {
-    case 0: ST_NP(0, kR0, kTile0); break;
-    case 1: ST_NP(1, 4, kTile12); break;
-    case 2: ST_NP(2, kR2, kTile12); break;
-    case 3: ST_NP(3, 8, kTile34); break;
-    default: ST_NP(4, 8, kTile34); break;
+    case 0: ST_NP(0, kR0, kTile0, lds); break;
+    case 1: ST_NP(1, 4, kTile12, lds); break;
+    case 2: ST_NP(2, kR2, kTile12, lds); break;
+    case 3: ST_NP(3, 8, kTile34, lds); break;
+    default: ST_NP(4, 8, kTile34, lds); break;
     }
   }
 #undef ST_NP
+#undef ST_NPS
 }
 
 template <typename T>
@@ -1403,6 +1446,20 @@ int
 st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype)
 {
   return st::round_flat_pays(nrows, ncols, dtype == 1 ? 8 : 4) ? 1 : 0;
+}
+
+int
+st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
+                  unsigned int wg_per_cu)
+{
+  st::clear_error();
+  if ((dtype != 0 && dtype != 1) || slot > (unsigned)st::kCapStore ||
+      (wg_per_cu == 1 || wg_per_cu > 32)) {
+    st::set_error("st_set_defer_caps: dtype 0/1, slot 0..6, cap 0 or 2..32");
+    return -1;
+  }
+  return (int)st::g_defer_caps[dtype][nontemporal != 0][slot].exchange(
+    wg_per_cu, std::memory_order_relaxed);
 }
 
 unsigned int

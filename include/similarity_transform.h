@@ -330,6 +330,16 @@ int st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype);
  * it. */
 unsigned int st_set_flat_grid_limit(unsigned int max_x);
 
+/* Workgroups per CU of the deferred flat round's launches (dtype 0 = f32,
+ * 1 = f64; nontemporal = the launch form of blocks >= 2 GiB, else the cached
+ * one; slot 0..4 = a read-only round with that many pending rounds, 6 =
+ * a storing round; wg_per_cu 0 = uncapped, else 2..32).  The library's
+ * defaults are measured (DESIGN.md §Deferred writes); this overrides one for
+ * the process, for tuning tools.  Results do not depend on it.  Returns the
+ * previous value, or -1 on bad arguments. */
+int st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
+                      unsigned int wg_per_cu);
+
 /* Round k of the flat round with deferred writes (what the solve loops run
  * for blocks where st_round_flat_pays): the matrix in d_mat is the last
  * STORED one, A_j; d_pend_s / d_pend_inv list the npend = k - j pending

@@ -160,3 +160,17 @@ def test_deferred_round_without_store_is_rejected_at_m_minus_1():
         assert rc < 0 and "without a store" in _lib.last_error()
         rc = fn(dummy, dummy, dummy, dummy, dummy, dummy, dummy, 8192, 8192, 0, 1e-3, 0, 1000, 0, arr, arr, m, 1, 0, dummy, None)
         assert rc < 0 and "pending rounds" in _lib.last_error()
+
+
+def test_defer_caps_setter():
+    """st_set_defer_caps (workgroups per CU of the deferred launches): bad
+    arguments are refused, a value set is returned by the next call (the
+    previous one), and the default is restored."""
+    L = _lib.load()
+    assert L.st_set_defer_caps(2, 0, 0, 4) < 0 and "st_set_defer_caps" in _lib.last_error()
+    assert L.st_set_defer_caps(1, 1, 7, 4) < 0
+    assert L.st_set_defer_caps(1, 1, 6, 1) < 0
+    assert L.st_set_defer_caps(1, 1, 6, 33) < 0
+    old = L.st_set_defer_caps(1, 1, 6, 5)
+    assert old >= 0
+    assert L.st_set_defer_caps(1, 1, 6, old) == 5

@@ -35,17 +35,38 @@ def rounds_per_store(n, elem, f64):
     return 6
 
 
+def set_caps(spec, dtype, n, elem):
+    """--caps a,b,c,d,e,f,g: workgroups per CU of the deferred launches
+    (slots 0..4 = read-only rounds by pending count, 6 = the storing round;
+    0 = uncapped) for this block's dtype and launch form (st_set_defer_caps)."""
+    from eigen_value_amd import _lib
+    L = _lib.load()
+    nt = 1 if n * n * elem >= (2 << 30) else 0
+    for slot, c in enumerate(int(x) for x in spec.split(",")):
+        if slot == 5:
+            continue
+        _lib.check(L.st_set_defer_caps(1 if dtype == "f64" else 0, nt, slot, c), "caps")
+
+
 def run(args):
     import torch
     import bench
     from eigen_value_amd import sharded
+    if args.caps:
+        set_caps(args.caps, args.dtype, args.n, 8 if args.dtype == "f64" else 4)
     dt = torch.float64 if args.dtype == "f64" else torch.float32
     sh = sharded.ShardedSimilarityTransform(args.n, dt)
     assert sh.deferred_writes, "block below the flat-round size: no deferred writes"
     sh.load(args.kind, seed=0)
     el, ev_ms, m = bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)
     out = {"workload": f"{args.kind}{args.n}_{args.dtype}", "m": m, "cycles": args.cycles,
-           "event_ms_per_round": ev_ms, "host_ms_per_round": el / (args.cycles * m) * 1e3}
+           "event_ms_per_round": ev_ms, "host_ms_per_round": el / (args.cycles * m) * 1e3,
+           "caps": args.caps}
+    if args.passes > 1:   # more passes over the same cycles (the first warmed up above)
+        more = [bench.timed_deferred(sh, args.cycles, 0, torch, None, 1)[1]
+                for _ in range(args.passes - 1)]
+        out["event_ms_per_round_passes"] = [ev_ms] + more
+        out["event_ms_per_round"] = sorted(out["event_ms_per_round_passes"])[len(more) // 2 + 0]
     print(json.dumps(out), flush=True)
     if args.events:
         json.dump(out, open(args.events, "w"), indent=1)
@@ -160,6 +181,9 @@ if __name__ == "__main__":
     p.add_argument("--launches", help="summary mode: write the per-launch rows (trimmed "
                                       "trace) here; the summary cites this file")
     p.add_argument("--fetch", help="with --write: summarise FETCH_SIZE / WRITE_SIZE passes")
+    p.add_argument("--caps", help="run mode: workgroups per CU of the deferred launches, "
+                                  "slots 0..6 comma-separated (st_set_defer_caps)")
+    p.add_argument("--passes", type=int, default=1, help="run mode: timed passes (median)")
     p.add_argument("--write")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4

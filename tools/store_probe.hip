@@ -207,7 +207,7 @@ report(const Block& b, const char* what, float ms, bool store)
 // the library's launch: k_flat fp64 (non-temporal, 4 KB pieces, or cached,
 // 8 KB pieces), FS stats, ALT, NP pending; `lds` bytes of dynamic LDS per
 // workgroup cap the workgroups per CU
-template <int R, int NP, bool NT = true>
+template <int R, int NP, bool NT = true, int DS = -1>
 static void
 lib_launch(const Block& b, int k, unsigned pt, bool store, unsigned lds = 0)
 {
@@ -223,7 +223,8 @@ lib_launch(const Block& b, int k, unsigned pt, bool store, unsigned lds = 0)
   pd.pt = pt;
   const unsigned ppr = b.n / (256 * W * U);
   const unsigned grid = b.nr / R * ppr;
-  hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NPK, U>),
+  hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NPK, U, false,
+                             DS>),
                      dim3(grid), dim3(256), lds, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, ppr,
                      0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
 }
@@ -243,7 +244,10 @@ static void
 cap_sweep(const Block& b)
 {
   const unsigned caps[] = { 0, 8, 6, 5, 4, 3, 2 };
+  const char* only = std::getenv("SP_ONLY");
   auto one = [&](const char* what, auto launch, bool store) {
+    if (only && !std::strstr(what, only))
+      return;
     for (unsigned c : caps) {
       const unsigned lds = lds_for(c);
       const float ms = time_seq([&](int k) { launch(k, lds); });
@@ -260,6 +264,8 @@ cap_sweep(const Block& b)
     one("NP=3 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 3, NT>(b, k, 16, false, l); }, false);
     one("NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, NT>(b, k, 16, false, l); }, false);
     one("store NP=5 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 0, true, l); }, true);
+    one("store NP=5 R=8 PT=0 DS=1", [&](int k, unsigned l) { lib_launch<8, 5, NT, 1>(b, k, 0, true, l); }, true);
+    one("store NP=5 R=8 PT=4 DS=1", [&](int k, unsigned l) { lib_launch<8, 5, NT, 1>(b, k, 4, true, l); }, true);
     one("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 4, true, l); }, true);
     one("store NP=5 R=4 PT=0", [&](int k, unsigned l) { lib_launch<4, 5, NT>(b, k, 0, true, l); }, true);
   } else {
@@ -269,6 +275,9 @@ cap_sweep(const Block& b)
     one("NP=1 R=4 PT=16", [&](int k, unsigned l) { lib_launch<4, 1, NT>(b, k, 16, false, l); }, false);
     one("NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, NT>(b, k, 16, false, l); }, false);
     one("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 4, true, l); }, true);
+    one("store NP=5 R=8 PT=4 DS=1", [&](int k, unsigned l) { lib_launch<8, 5, NT, 1>(b, k, 4, true, l); }, true);
+    one("NP=2 R=4 PT=16", [&](int k, unsigned l) { lib_launch<4, 2, NT>(b, k, 16, false, l); }, false);
+    one("NP=3 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 3, NT>(b, k, 16, false, l); }, false);
   }
 }
 
