@@ -35,17 +35,51 @@ def rounds_per_store(n, elem, f64):
     return 6
 
 
-def set_caps(spec, dtype, n, elem):
+def set_caps(spec, dtype, n, elem, nrows=None):
     """--caps a,b,c,d,e,f,g: workgroups per CU of the deferred launches
     (slots 0..4 = read-only rounds by pending count, 6 = the storing round;
     0 = uncapped) for this block's dtype and launch form (st_set_defer_caps)."""
     from eigen_value_amd import _lib
     L = _lib.load()
-    nt = 1 if n * n * elem >= (2 << 30) else 0
+    nt = 1 if (nrows or n) * n * elem >= (2 << 30) else 0
     for slot, c in enumerate(int(x) for x in spec.split(",")):
         if slot == 5:
             continue
         _lib.check(L.st_set_defer_caps(1 if dtype == "f64" else 0, nt, slot, c), "caps")
+
+
+def run_caps_ab(args):
+    """--caps-ab 'spec;spec;...': the same store cycles under each caps spec
+    (st_set_defer_caps), interleaved over --passes repeats so that clock
+    drift hits every spec alike; prints and returns the median ms per round
+    of each spec."""
+    import torch
+    import bench
+    from eigen_value_amd import sharded
+    elem = 8 if args.dtype == "f64" else 4
+    dt = torch.float64 if args.dtype == "f64" else torch.float32
+    rb = (args.rank_block, 0) if args.rank_block else None
+    sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb)
+    assert sh.deferred_writes
+    sh.load(args.kind, seed=0)
+    specs = args.caps_ab.split(";")
+    res = {sp: [] for sp in specs}
+    set_caps(specs[0], args.dtype, args.n, elem, sh.part.nrows)
+    bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)          # warm-up
+    for _ in range(args.passes):
+        for sp in specs:
+            set_caps(sp, args.dtype, args.n, elem, sh.part.nrows)
+            res[sp].append(bench.timed_deferred(sh, args.cycles, 0, torch, None, 1)[1])
+    out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
+               f" rank 0 of {args.rank_block}" if args.rank_block else ""),
+           "cycles": args.cycles, "passes": args.passes, "ms_per_round": {}}
+    for sp in specs:
+        v = sorted(res[sp])
+        out["ms_per_round"][sp] = {"median": v[len(v) // 2], "min": v[0], "max": v[-1]}
+        print(f"{out['workload']} caps {sp:24s} median {v[len(v) // 2]:.5f} ms/round "
+              f"(min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
+    sh.close()
+    return out
 
 
 def run(args):
@@ -184,12 +218,20 @@ if __name__ == "__main__":
     p.add_argument("--caps", help="run mode: workgroups per CU of the deferred launches, "
                                   "slots 0..6 comma-separated (st_set_defer_caps)")
     p.add_argument("--passes", type=int, default=1, help="run mode: timed passes (median)")
+    p.add_argument("--caps-ab", help="A/B of caps specs separated by ';' (interleaved passes)")
+    p.add_argument("--ab-json", help="with --caps-ab: write the medians here")
+    p.add_argument("--rank-block", type=int, default=0,
+                   help="with --caps-ab: rank 0's block of a P-way row partition (no exchange)")
     p.add_argument("--write")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.trace or a.fetch:
+    if a.caps_ab:
+        r = run_caps_ab(a)
+        if a.ab_json:
+            json.dump(r, open(a.ab_json, "w"), indent=1)
+    elif a.trace or a.fetch:
         res = {}
         if a.trace:
             res = summarise(a.trace, a.n, elem, m, wl, a.events, a.launches)

@@ -65,6 +65,18 @@ for s in $STEPS; do
     longrow) # configs[3]'s long-row rank blocks: column-block piece orders + the counter list
       rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
       FMS_EVERY=1 FMS_PT=4 FMS_PC=0,16,32,64 step longrow_pc 600 ./tools/flat_map_sweep f64 32768 8192x65536 16384x65536 ;;
+    capsab) # workgroups-per-CU caps of the deferred launches, A/B in the solve loop
+      NT_SPECS="0,0,0,0,0,0,0;0,0,0,0,0,0,3;0,6,5,4,5,0,3;0,5,4,4,4,0,3;0,6,5,4,5,0,4"
+      C_SPECS="0,0,0,0,0,0,0;0,4,0,0,3,0,0;0,4,4,4,3,0,0;0,5,5,4,4,0,0;0,4,4,4,3,0,3"
+      step capsab_f64_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/capsab_random32768_f64.json"
+      step capsab_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/capsab_random32768_f32.json"
+      step capsab_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/capsab_random65536_p8_f64.json"
+      step capsab_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/capsab_hilbert8192_f64.json"
+      step capsab_f32_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f32 --cycles 60 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/capsab_hilbert8192_f32.json" ;;
+    storeprobe) # the storing round's shapes and caps (tools/store_probe)
+      make -s -C tools store_probe
+      SP_CAPS=1 SP_ONLY=store step storeprobe_nt 300 ./tools/store_probe 32768 8192x65536
+      SP_CAPS=1 SP_CACHED=1 step storeprobe_cached 200 ./tools/store_probe 8192 ;;
     defer) # the deferred-write rounds over whole store cycles: rocprof + HIP events
       for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
         set -- $W; K=$1; N=$2; DT=$3; D="$OUT/defer_${K}${N}_${DT}"; mkdir -p "$D"
