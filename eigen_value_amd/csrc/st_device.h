@@ -1141,9 +1141,10 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // NP = 4, 8 rows, tiles of 16: 1.23 vs 1.29 ms; the storing round with 5
   // pending and fp32 lose 1 - 2 %, their merged scales crowd the SGPRs)
   const T* rs = NP >= 0 ? pend.inv_cur : s_cur;
-  // (the storing round merges its row loads only with its store decision
-  // fixed at compile time, DS = 1: tools/store_probe, profiles/r03_store_probe*)
-  constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && (NP <= 4 || DS == 1);
+  // (not the storing round with 5 pending: 2.895 vs 2.853 ms at 32768^2
+  // fp64 with its store decision fixed at compile time too,
+  // profiles/r03_store_probe_caps_nt.log "DS=1")
+  constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && NP <= 4;
   if (kMergeRows && r0 + R <= nrows) { // uniform
 #pragma unroll
     for (int j = 0; j < R; j++)

@@ -706,16 +706,23 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 // flight oversubscribes the memory system at full occupancy (5-6
 // workgroups, up to 192 KB of loads per CU): capping it - with dynamic LDS
 // the kernel does not use, the only hard cap on workgroups per CU - is
-// faster (tools/store_probe SP_CAPS=1, profiles/r03_store_probe_caps_*.log:
-// the non-temporal storing round 2.85 -> 2.77 ms at 3 per CU, 32768^2
-// fp64).  Indexed [fp64][non-temporal][slot], slot = the pending count of a
-// read-only round (0 ... 4) or kCapStore for a storing one.
+// faster: single launches (tools/store_probe SP_CAPS=1,
+// profiles/r03_store_probe_caps_*.log) the non-temporal storing round 2.85
+// -> 2.78 ms at 3 per CU (32768^2 fp64), NP = 3 1.205 -> 1.183 at 4; the
+// R = 2 launches (every-round, NP = 0) only lose.  The solve loop over whole
+// store cycles (tools/defer_profile.py --caps-ab, 5 interleaved passes,
+// profiles/r03_capsab_*.json) picks the table: 32768^2 fp64 1.483 vs 1.510
+// ms per round, the P = 8 rank block of configs[3] 0.767 vs 0.782, 32768^2
+// fp32 0.733 vs 0.744, 8192^2 fp64 0.1008 vs 0.1024; cached fp32 blocks lose
+// with any cap (8192^2 0.0486 uncapped, 0.050 - 0.055 capped).  Indexed
+// [fp64][non-temporal][slot], slot = the pending count of a read-only round
+// (0 ... 4) or kCapStore for a storing one (5 unused).
 constexpr int kCapStore = 6;
 std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   // fp32: cached, non-temporal
-  { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 0, 0, 0, 0, 0, 0 } },
+  { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 6, 5, 4, 5, 0, 3 } },
   // fp64: cached, non-temporal
-  { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 0, 0, 0, 0, 0, 0 } },
+  { { 0, 4, 4, 4, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
 // dynamic LDS that leaves room for `cap` workgroups per CU (160 KB of LDS

@@ -73,6 +73,23 @@ for s in $STEPS; do
       step capsab_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/capsab_random65536_p8_f64.json"
       step capsab_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/capsab_hilbert8192_f64.json"
       step capsab_f32_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f32 --cycles 60 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/capsab_hilbert8192_f32.json" ;;
+    capsab2) # the shipped caps table against no caps and its neighbours
+      NT_SPECS="0,5,4,4,4,0,3;0,0,0,0,0,0,0;0,5,4,4,5,0,3;0,6,4,4,4,0,3;0,5,4,4,4,0,4"
+      C_SPECS="0,4,4,4,3,0,3;0,0,0,0,0,0,0;0,4,4,4,3,0,4;0,4,4,3,3,0,3;0,5,4,4,3,0,3"
+      F32_SPECS="0,6,5,4,5,0,3;0,0,0,0,0,0,0;0,5,4,4,4,0,3;0,6,5,4,5,0,4"
+      step capsab2_f64_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/${RTAG}_capsab2_random32768_f64.json"
+      step capsab2_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/${RTAG}_capsab2_random65536_p8_f64.json"
+      step capsab2_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 5 --caps-ab "$F32_SPECS" --ab-json "$OUT/${RTAG}_capsab2_random32768_f32.json"
+      step capsab2_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab2_hilbert8192_f64.json" ;;
+    sq) # SQ instruction / wait counters of the deferred launches (two PMC passes)
+      C1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
+      C2="SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"
+      for W in "random 32768 f64" "hilbert 8192 f64"; do
+        set -- $W; D="$OUT/sq_$1$2_$3"; mkdir -p "$D"
+        step "sq1_$1$2" 120 rocprofv3 --pmc $C1 --output-format csv -d "$D/p1" -o run -- python3 tools/defer_profile.py --kind $1 --n $2 --dtype $3 --cycles 2
+        step "sq2_$1$2" 120 rocprofv3 --pmc $C2 --output-format csv -d "$D/p2" -o run -- python3 tools/defer_profile.py --kind $1 --n $2 --dtype $3 --cycles 2
+        python3 tools/sq_counters.py "$D/p1/run_counter_collection.csv" "$D/p2/run_counter_collection.csv" --json="$OUT/${RTAG}_sq_counters_defer_$1$2_$3.json" | tee -a "$OUT/session.log"
+      done ;;
     storeprobe) # the storing round's shapes and caps (tools/store_probe)
       make -s -C tools store_probe
       SP_CAPS=1 SP_ONLY=store step storeprobe_nt 300 ./tools/store_probe 32768 8192x65536
