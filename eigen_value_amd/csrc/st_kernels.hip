@@ -714,7 +714,11 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 // profiles/r03_capsab_*.json) picks the table: 32768^2 fp64 1.483 vs 1.510
 // ms per round, the P = 8 rank block of configs[3] 0.767 vs 0.782, 32768^2
 // fp32 0.733 vs 0.744, 8192^2 fp64 0.1008 vs 0.1024; cached fp32 blocks lose
-// with any cap (8192^2 0.0486 uncapped, 0.050 - 0.055 capped).  Indexed
+// with any cap (8192^2 0.0486 uncapped, 0.050 - 0.055 capped).  A second
+// A/B of the table against its neighbours (profiles/r03_capsab2_*.json):
+// P = 8 rank block 0.759 vs 0.777 uncapped, 8192^2 fp64 0.0995 (NP = 3 at 3
+// per CU) vs 0.1013; 32768^2 fp64 within the box's noise that run (min
+// 1.485 vs 1.503 uncapped).  Indexed
 // [fp64][non-temporal][slot], slot = the pending count of a read-only round
 // (0 ... 4) or kCapStore for a storing one (5 unused).
 constexpr int kCapStore = 6;
@@ -722,7 +726,7 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   // fp32: cached, non-temporal
   { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 6, 5, 4, 5, 0, 3 } },
   // fp64: cached, non-temporal
-  { { 0, 4, 4, 4, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
+  { { 0, 4, 4, 3, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
 // dynamic LDS that leaves room for `cap` workgroups per CU (160 KB of LDS

@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""List the files under profiles/ that no document, test, tool or bench
+code cites (README.md, profiles/README.md, INTEGRATION.md,
+bench.py, tests/, tools/, eigen_value_amd/).  Citations may use shell
+patterns (`r02_flat_map_every_*.log`, `r02_defer_pmc_random32768_{f64,f32}.json`),
+which are expanded against the directory.
+
+    python3 tools/check_citations.py          # prints the uncited files
+    python3 tools/check_citations.py --rm     # and removes them (git rm)
+"""
+import fnmatch
+import glob
+import itertools
+import os
+import re
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SOURCES = ["DESIGN.md", "README.md", "INTEGRATION.md", "profiles/README.md", "bench.py",
+           "tests/*.py", "tools/*.py", "tools/*.hip", "tools/*.sh", "tools/*.cpp",
+           "eigen_value_amd/*.py", "eigen_value_amd/csrc/*", "include/*.h"]
+TOKEN = re.compile(r"r0\d_[A-Za-z0-9_*{},.\-\[\]]+")
+
+
+def braces(p):
+    """Expand {a,b} alternatives (no nesting)."""
+    m = re.search(r"\{([^{}]*)\}", p)
+    if not m:
+        return [p]
+    return list(itertools.chain.from_iterable(
+        braces(p[:m.start()] + alt + p[m.end():]) for alt in m.group(1).split(",")))
+
+
+def cited_patterns():
+    pats = set()
+    for pat in SOURCES:
+        for f in glob.glob(os.path.join(HERE, pat)):
+            if os.path.isfile(f):
+                for tok in TOKEN.findall(open(f, errors="replace").read()):
+                    tok = tok.rstrip(".,")
+                    for p in braces(tok):
+                        pats.add(p)
+    return pats
+
+
+def uncited():
+    files = sorted(os.listdir(os.path.join(HERE, "profiles")))
+    pats = cited_patterns()
+    out = []
+    for f in files:
+        if f == "README.md":
+            continue
+        stem = os.path.splitext(f)[0]
+        hit = any(fnmatch.fnmatch(f, p) or fnmatch.fnmatch(stem, p) or f.startswith(p)
+                  or (("*" in p or "?" in p) and fnmatch.fnmatch(f, p + "*"))
+                  for p in pats)
+        if not hit:
+            out.append(f)
+    return out
+
+
+if __name__ == "__main__":
+    left = uncited()
+    for f in left:
+        print(f"profiles/{f}")
+    if "--rm" in sys.argv and left:
+        subprocess.run(["git", "rm", "-q", *[f"profiles/{f}" for f in left]], cwd=HERE,
+                       check=True)
