@@ -64,7 +64,16 @@ for s in $STEPS; do
       step bench_spawn_p8 900 python bench.py --gpus 8 --one-gpu --backend gloo --steps 5 --warmup 1 ;;
     longrow) # configs[3]'s long-row rank blocks: column-block piece orders + the counter list
       rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
-      FMS_EVERY=1 FMS_PT=4 FMS_PC=0,16,32,64 step longrow_pc 600 ./tools/flat_map_sweep f64 32768 8192x65536 16384x65536 ;;
+      FMS_EVERY=1 FMS_PT=4 FMS_PC=0,16,32,64 step longrow_pc 600 ./tools/flat_map_sweep f64 32768 8192x65536 16384x65536
+      # translation and address-unit counters of the every-round launch, square vs long rows
+      for SZ in 32768 8192x65536; do
+        D="$OUT/longrow_pmc_$SZ"; mkdir -p "$D"
+        FMS_EVERY=1 FMS_PT=4 step "lr_tcp_$SZ" 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_REQUEST_sum TCP_TCC_READ_REQ_sum --output-format csv -d "$D/tcp" -o run -- ./tools/flat_map_sweep f64 $SZ || true
+        FMS_EVERY=1 FMS_PT=4 step "lr_ta_$SZ" 120 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VALU SQ_BUSY_CYCLES --output-format csv -d "$D/sq" -o run -- ./tools/flat_map_sweep f64 $SZ || true
+        for P in tcp sq; do
+          [ -f "$D/$P/run_counter_collection.csv" ] && python3 tools/sq_counters.py "$D/$P/run_counter_collection.csv" --json="$OUT/${RTAG}_longrow_${P}_$SZ.json" | tee -a "$OUT/session.log"
+        done
+      done ;;
     capsab) # workgroups-per-CU caps of the deferred launches, A/B in the solve loop
       NT_SPECS="0,0,0,0,0,0,0;0,0,0,0,0,0,3;0,6,5,4,5,0,3;0,5,4,4,4,0,3;0,6,5,4,5,0,4"
       C_SPECS="0,0,0,0,0,0,0;0,4,0,0,3,0,0;0,4,4,4,3,0,0;0,5,5,4,4,0,0;0,4,4,4,3,0,3"
@@ -90,6 +99,9 @@ for s in $STEPS; do
         step "sq2_$1$2" 120 rocprofv3 --pmc $C2 --output-format csv -d "$D/p2" -o run -- python3 tools/defer_profile.py --kind $1 --n $2 --dtype $3 --cycles 2
         python3 tools/sq_counters.py "$D/p1/run_counter_collection.csv" "$D/p2/run_counter_collection.csv" --json="$OUT/${RTAG}_sq_counters_defer_$1$2_$3.json" | tee -a "$OUT/session.log"
       done ;;
+    pipe) # the software-pipelined deferred kernel (k_pipe) against k_flat, with a bitwise check
+      make -s -C tools store_probe
+      SP_CHECK=1 SP_PIPE=1 step pipe_probe 400 ./tools/store_probe 32768 8192x65536 ;;
     storeprobe) # the storing round's shapes and caps (tools/store_probe)
       make -s -C tools store_probe
       SP_CAPS=1 SP_ONLY=store step storeprobe_nt 300 ./tools/store_probe 32768 8192x65536

@@ -7,7 +7,8 @@ rocprofv3 --pmc passes (counter_collection.csv files, any number):
 Prints, per k_flat NP (-1 = every-round store, m - 1 = the storing round)
 and k_parts: instructions per wave (VALU, SALU, SMEM, VMEM), the wave's
 cycles split into active / waiting on memory / issue-stalled, VGPR and
-SGPR counts."""
+SGPR counts.  Passes without SQ_WAVES (e.g. TCP / TA counters) print their
+per-dispatch values instead."""
 import collections
 import csv
 import json
@@ -46,7 +47,7 @@ def main(paths):
         if waves:
             row["per_wave"] = {n: round(v / waves, 1) for n, v in per.items() if n != "SQ_WAVES"}
         out[k] = row
-        pw = row.get("per_wave", {})
+        pw = row.get("per_wave") or {n: round(v, 1) for n, v in per.items()}
         print(f"{k:40s} v/s {regs[k]}  " + "  ".join(f"{n.replace('SQ_', '')}={v}"
                                                     for n, v in sorted(pw.items())))
     return out

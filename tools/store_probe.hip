@@ -27,6 +27,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "st_device.h"
@@ -140,6 +141,100 @@ k_sp(T* a, const T* __restrict__ s_cur, const T* __restrict__ inv_cur, T* __rest
     else if constexpr (STORE)
       *reinterpret_cast<V*>(wrow + (size_t)j * ncols) = y;
     acc[j] = hsum<T, W>(y);
+  }
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j + 1 < R; j += 2) {
+    const T t = wave_sum_pair(acc[j], acc[j + 1]);
+    if (lane >= 62)
+      red[wave][j + (lane - 62)] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < R) {
+    T t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; w++)
+      t += red[w][threadIdx.x];
+    part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+  }
+}
+
+// k_pipe: R = RB * NB rows per workgroup walked in NB steps of RB rows, the
+// next step's matrix loads issued before the current step's math and stores
+// (double-buffered registers; sched_barrier keeps the order), so a
+// workgroup keeps loads in flight through its compute; the column scales
+// load once for the R rows, the row scales per step (scalar, unconditional).
+// Element math, row sums and partials as k_flat (bitwise).
+template <int RB, int NB, int NP, bool STORE>
+__global__ __launch_bounds__(BLK) void
+k_pipe(T* a, const T* __restrict__ s_cur, const T* __restrict__ inv_cur, T* __restrict__ part,
+       uint32_t nrows, uint32_t ncols, uint32_t ppr, uint32_t pt, const st_state* state,
+       uint32_t k, Pend<NP> pend)
+{
+  constexpr int R = RB * NB;
+  if (flat_gated<kGatePlain>(state, k))
+    return;
+  __shared__ T red[NW][R];
+  uint32_t rg, p;
+  sp_map(blockIdx.x, ppr, nrows / R, pt, rg, p);
+  const uint32_t r0 = rg * R;
+  const uint32_t c0 = (p * BLK + threadIdx.x) * W;
+  const T* ap = a + (size_t)r0 * ncols + c0;
+  T* wp = a + (size_t)r0 * ncols + c0;
+  V xa[RB], xb[RB];
+#pragma unroll
+  for (int j = 0; j < RB; j++)
+    xa[j] = __builtin_nontemporal_load(reinterpret_cast<const V*>(ap + (size_t)j * ncols));
+  const V sc = *reinterpret_cast<const V*>(s_cur + c0);
+  V spc[NP > 0 ? NP : 1];
+#pragma unroll
+  for (int i = 0; i < NP; i++)
+    spc[i] = *reinterpret_cast<const V*>(pend.s[i] + c0);
+  T acc[R];
+  auto load = [&](V (&x)[RB], int step) {
+#pragma unroll
+    for (int j = 0; j < RB; j++)
+      x[j] = __builtin_nontemporal_load(
+        reinterpret_cast<const V*>(ap + (size_t)(step * RB + j) * ncols));
+  };
+  auto work = [&](V (&x)[RB], int step) {
+    const uint32_t rr = r0 + step * RB;
+    T sr[NP + 1][RB];
+#pragma unroll
+    for (int i = 0; i <= NP; i++) {
+      const T* src = i < NP ? pend.inv[i < NP ? i : 0] : inv_cur;
+#pragma unroll
+      for (int j = 0; j < RB; j++)
+        sr[i][j] = src[rr + j];
+    }
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+#pragma unroll
+      for (int j = 0; j < RB; j++)
+        x[j] = x[j] * (sr[i][j] * spc[i]);
+    }
+#pragma unroll
+    for (int j = 0; j < RB; j++) {
+      const V y = x[j] * (sr[NP][j] * sc); // cpp:324-325
+      if constexpr (STORE)
+        __builtin_nontemporal_store(
+          y, reinterpret_cast<V*>(wp + (size_t)(step * RB + j) * ncols));
+      acc[step * RB + j] = hsum<T, W>(y);
+    }
+  };
+#pragma unroll
+  for (int st = 0; st < NB; st += 2) {
+    if (st + 1 < NB)
+      load(xb, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
+    work(xa, st);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 2 < NB)
+      load(xa, st + 2);
+    __builtin_amdgcn_sched_barrier(0);
+    if (st + 1 < NB)
+      work(xb, st + 1);
+    __builtin_amdgcn_sched_barrier(0);
   }
   const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
@@ -310,6 +405,34 @@ sp_time(const Block& b, unsigned pt)
 
 static std::vector<unsigned> g_pts = { 0, 4, 16 };
 
+template <int RB, int NB, int NP, bool STORE>
+static void
+pipe_launch(const Block& b, int k, unsigned pt, unsigned lds)
+{
+  Pend<NP> pd{};
+  for (int i = 0; i < NP; i++) {
+    pd.s[i] = b.s[1 + i];
+    pd.inv[i] = b.inv[1 + i];
+  }
+  const unsigned grid = b.nr / (RB * NB) * b.ppr;
+  hipLaunchKernelGGL((k_pipe<RB, NB, NP, STORE>), dim3(grid), dim3(BLK), lds, 0, b.a,
+                     b.s[0], b.inv[0], b.part, b.nr, b.n, b.ppr, pt, b.st, (uint32_t)k, pd);
+}
+
+template <int RB, int NB, int NP, bool STORE>
+static void
+pipe_time(const Block& b, unsigned pt, unsigned cap)
+{
+  const unsigned lds = lds_for(cap);
+  const float ms = time_seq([&](int k) { pipe_launch<RB, NB, NP, STORE>(b, k, pt, lds); });
+  char w[96];
+  std::snprintf(w, sizeof w, "k_pipe NP=%d %s RB=%d NB=%d PT=%u cap=%u", NP,
+                STORE ? "store" : "read", RB, NB, pt, cap);
+  report(b, w, ms, STORE);
+}
+
+
+
 static void
 run(unsigned nr, unsigned n, bool check)
 {
@@ -350,18 +473,23 @@ run(unsigned nr, unsigned n, bool check)
     HIPCHECK(hipMemcpy(ra.data(), b.a, bytes, hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(rp.data(), b.part, np * sizeof(T), hipMemcpyDeviceToHost));
     bool ok = true;
-    for (int rs = 0; rs < 2; rs++) {
+    for (int rs = 0; rs < 4; rs++) {
       HIPCHECK(hipMemcpy(b.a, a0.data(), bytes, hipMemcpyHostToDevice));
       HIPCHECK(hipMemset(b.part, 0, np * sizeof(T)));
       if (rs == 0)
         sp_launch<8, 5, 0, true>(b, 0, 16);
-      else
+      else if (rs == 1)
         sp_launch<8, 5, 1, true>(b, 0, 16);
+      else if (rs == 2)
+        pipe_launch<2, 4, 5, true>(b, 0, 4, 0);
+      else
+        pipe_launch<4, 2, 5, true>(b, 0, 0, lds_for(3));
       HIPCHECK(hipMemcpy(xa.data(), b.a, bytes, hipMemcpyDeviceToHost));
       HIPCHECK(hipMemcpy(xp.data(), b.part, np * sizeof(T), hipMemcpyDeviceToHost));
       const bool same = std::memcmp(ra.data(), xa.data(), bytes) == 0 &&
                         std::memcmp(rp.data(), xp.data(), np * sizeof(T)) == 0;
-      std::printf("  check k_sp RS=%d vs k_flat NP=5 store: %s\n", rs,
+      std::printf("  check %s vs k_flat NP=5 store: %s\n",
+                  rs == 0 ? "k_sp RS=0" : rs == 1 ? "k_sp RS=1" : rs == 2 ? "k_pipe 2x4" : "k_pipe 4x2",
                   same ? "bitwise equal" : "DIFFERENT");
       ok = ok && same;
     }
@@ -377,7 +505,22 @@ run(unsigned nr, unsigned n, bool check)
     report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
            time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
   }
-  if (std::getenv("SP_CAPS")) { // the library's shapes under workgroup-per-CU caps
+  if (std::getenv("SP_PIPE")) { // the software-pipelined k_pipe against k_flat (capped)
+    for (unsigned cap : { 0u, 4u, 3u }) {
+      report(b, (std::string("k_flat store NP=5 R=8 PT=0 cap=") + std::to_string(cap)).c_str(),
+             time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true, lds_for(cap)); }), true);
+      report(b, (std::string("k_flat read NP=4 R=8 PT=16 cap=") + std::to_string(cap)).c_str(),
+             time_seq([&](int k) { lib_launch<8, 4>(b, k, 16, false, lds_for(cap)); }), false);
+    }
+    for (unsigned pt : { 0u, 4u, 16u })
+      for (unsigned cap : { 0u, 6u, 4u, 3u }) {
+        pipe_time<2, 4, 5, true>(b, pt, cap);
+        pipe_time<4, 2, 5, true>(b, pt, cap);
+        pipe_time<2, 2, 5, true>(b, pt, cap);
+        pipe_time<2, 4, 4, false>(b, pt, cap);
+        pipe_time<4, 2, 4, false>(b, pt, cap);
+      }
+  } else if (std::getenv("SP_CAPS")) { // the library's shapes under workgroup-per-CU caps
     if (std::getenv("SP_CACHED"))
       cap_sweep<false>(b);
     else
