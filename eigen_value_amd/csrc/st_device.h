@@ -1379,6 +1379,52 @@ k_parts_t(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   }
 }
 
+// k_parts for rows of at most LPR (16 or 32) partials: 64 / LPR rows per
+// wave, LPR lanes each (4x / 2x fewer waves than k_parts).  Bitwise
+// k_parts' sums: in k_parts' one-row wave the lanes past ppr hold 0, so its
+// rows of 16 (LPR = 16) or half-waves (LPR = 32) past the first carry 0 and
+// the tree's later steps add exact zeros - lane 15 after the row_ror steps
+// (LPR = 16) / lane 31 after row_bcast 15 (LPR = 32) already holds
+// wave_sum's value, bit for bit.  Here those segments hold other rows, and
+// the tree stops there.
+template <typename T, int LPR, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_parts_seg(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
+            uint32_t ppr /* <= LPR */, uint32_t k, const st_state* state,
+            const T* __restrict__ s_cur, T* __restrict__ v, uint32_t row0,
+            T* __restrict__ inv_next)
+{
+  static_assert(LPR == 16 || LPR == 32, "segments of 16 or 32 lanes");
+  const uint32_t seg = threadIdx.x % LPR;
+  const uint32_t r = (blockIdx.x * BLK + threadIdx.x) / LPR;
+  // whole waves stay together (DPP reads neighbours): rows past the block
+  // compute on zeros and store nothing
+  const bool live = r < nrows;
+  const uint32_t e = state->end;
+  T vr = (T)0, sr = (T)1, m = (T)1;
+  if (v != nullptr && seg == LPR - 1 && live) {
+    vr = v[row0 + r];
+    sr = s_cur[row0 + r];
+    m = (T)state->max;
+  }
+  T x = (live && seg < ppr) ? part[(size_t)r * ppr + seg] : (T)0;
+  x += dpp_mov<0xB1>(x);       // quad_perm [1,0,3,2]
+  x += dpp_mov<0x4E>(x);       // quad_perm [2,3,0,1]
+  x += dpp_mov<0x124>(x);      // row_ror 4
+  x += dpp_mov<0x128>(x);      // row_ror 8
+  if constexpr (LPR == 32)
+    x += dpp_mov<0x142, 0xa>(x); // row_bcast 15 (rows 1 and 3)
+  if (e != 0 && e <= k)
+    return;
+  if (seg == LPR - 1 && live) {
+    s_next[r] = x;
+    if (inv_next != nullptr)
+      inv_next[r] = (T)1 / x;
+    if (v != nullptr)
+      v[row0 + r] = vr * (sr / m); // cpp:260
+  }
+}
+
 template <typename T, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,

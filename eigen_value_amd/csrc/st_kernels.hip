@@ -246,6 +246,30 @@ flat_every_tile(uint32_t nrows, uint32_t ncols)
   return block_bytes(nrows, ncols, sizeof(T)) >= ((size_t)384 << 20) ? 8u : 4u;
 }
 
+// k_parts of an unsplit flat round: rows of <= 16 / 32 partials take 4 / 2
+// rows per wave (k_parts_seg, bitwise k_parts' sums), longer ones a wave
+// each (k_parts)
+template <typename T>
+void
+launch_parts(const T* part, T* s_next, uint32_t nrows, uint32_t ppr, uint32_t k,
+             const st_state* st, const T* s_cur, T* v, uint32_t row0, T* inv_next,
+             hipStream_t stream)
+{
+  if (ppr <= 16) {
+    const uint32_t g = (nrows + kBlock / 16 - 1) / (kBlock / 16);
+    hipLaunchKernelGGL((dev::k_parts_seg<T, 16>), dim3(g), dim3(kBlock), 0, stream, part,
+                       s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next);
+  } else if (ppr <= 32) {
+    const uint32_t g = (nrows + kBlock / 32 - 1) / (kBlock / 32);
+    hipLaunchKernelGGL((dev::k_parts_seg<T, 32>), dim3(g), dim3(kBlock), 0, stream, part,
+                       s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next);
+  } else {
+    const uint32_t g = (nrows + dev::kWaves - 1) / dev::kWaves;
+    hipLaunchKernelGGL((dev::k_parts<T>), dim3(g), dim3(kBlock), 0, stream, part, s_next,
+                       nrows, ppr, k, st, s_cur, v, row0, nullptr, 0u, 0u, 0u, inv_next);
+  }
+}
+
 // partial sums per row (one per piece) and the scratch they need
 inline uint32_t
 flat_pieces(uint32_t ncols, int w)
@@ -594,8 +618,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
       fg.grid,
       dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
       st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
-    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
-                       part, s_next, nrows, ppr, k, st, s_cur, v, row0);
+    launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr, stream);
   } else {
     const uint32_t sgrid =
       (ncols + kBlock - 1) / kBlock < 256u ? (ncols + kBlock - 1) / kBlock : 256u;
@@ -677,7 +700,6 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
   const uint32_t grid = (nrows + R - 1) / R * ppr;
-  const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   dev::FlatPending<T, NP> pd{};
   for (int i = 0; i < NP; i++) {
     pd.s[i] = pend_s[i];
@@ -696,9 +718,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
   if (!flush) // a flush only stores the matrix: s, v and the state stand
-    hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
-                       part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr,
-                       0u, 0u, 0u, inv_next);
+    launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next, stream);
 }
 
 // Workgroups per CU of the deferred rounds' launches (0 = as many as the
