@@ -993,6 +993,22 @@ def test_wave_reductions_bitwise():
     assert "wave reductions bit-identical" in out.stdout
 
 
+def test_parts_segments_bitwise():
+    """tests/cpp/test_parts.hip: k_parts_seg (4 / 2 rows per wave for rows of
+    at most 16 / 32 partials, the flat round's partial-sum launch on cached
+    and short blocks) against k_parts (a wave per row): s_{k+1}, 1/s_{k+1}
+    and the eigenvector update bit for bit, every partial count 1 ... 32,
+    row counts that leave waves partly empty, fp64 and fp32."""
+    import subprocess
+    here = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run(["make", "-s", "-C", os.path.join(here, "cpp"), "test_parts"], check=True)
+    out = subprocess.run([os.path.join(here, "cpp", "test_parts")], capture_output=True,
+                         text=True, timeout=120)
+    print(out.stdout)
+    assert out.returncode == 0, out.stdout + out.stderr
+    assert "k_parts_seg bit-identical to k_parts" in out.stdout
+
+
 # ---------------------------------------------------------------------------
 # the whole solve in one workgroup (k_solve_small, n <= 128 fp64 / 256 fp32)
 # against the per-round launch loop: bit-identical λ, v, iteration count and
