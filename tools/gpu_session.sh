@@ -99,6 +99,8 @@ for s in $STEPS; do
         step "sq2_$1$2" 120 rocprofv3 --pmc $C2 --output-format csv -d "$D/p2" -o run -- python3 tools/defer_profile.py --kind $1 --n $2 --dtype $3 --cycles 2
         python3 tools/sq_counters.py "$D/p1/run_counter_collection.csv" "$D/p2/run_counter_collection.csv" --json="$OUT/${RTAG}_sq_counters_defer_$1$2_$3.json" | tee -a "$OUT/session.log"
       done ;;
+    weakshape) # piece size (4 / 8 KB) of the every-round launch on the weak-scaled rank blocks
+      FMS_EVERY=1 FMS_U1=1 FMS_PT=0,4,8 step weakshape 400 ./tools/flat_map_sweep f64 8192 5824x11648 4096x16384 2880x23040 ;;
     pipe) # the software-pipelined deferred kernel (k_pipe) against k_flat, with a bitwise check
       make -s -C tools store_probe
       SP_CHECK=1 SP_PIPE=1 step pipe_probe 400 ./tools/store_probe 32768 8192x65536 ;;
