@@ -106,9 +106,59 @@ run_case(const char* name, uint32_t nrows, uint32_t ppr, uint32_t seed)
   return ok ? 0 : 1;
 }
 
+// launch time of k_parts vs k_parts_seg (printed, not asserted): rows of
+// the configs[1] flat round (8192 rows x 8 partials) and the N = 2 rank
+// block (5824 x 12)
+template <typename T>
+static int
+time_case(uint32_t nrows, uint32_t ppr)
+{
+  T *d_part, *d_s, *d_scur, *d_v, *d_inv;
+  st_state* d_st;
+  HIPCHECK(hipMalloc(&d_part, sizeof(T) * nrows * ppr));
+  HIPCHECK(hipMemset(d_part, 0, sizeof(T) * nrows * ppr));
+  HIPCHECK(hipMalloc(&d_s, sizeof(T) * nrows));
+  HIPCHECK(hipMalloc(&d_inv, sizeof(T) * nrows));
+  HIPCHECK(hipMalloc(&d_scur, sizeof(T) * nrows));
+  HIPCHECK(hipMalloc(&d_v, sizeof(T) * nrows));
+  HIPCHECK(hipMalloc(&d_st, sizeof(st_state)));
+  HIPCHECK(hipMemset(d_st, 0, sizeof(st_state)));
+  hipEvent_t e0, e1;
+  HIPCHECK(hipEventCreate(&e0));
+  HIPCHECK(hipEventCreate(&e1));
+  float ms[2];
+  for (int which = 0; which < 2; which++) {
+    for (int rep = 0; rep < 2; rep++) { // warm-up pass, then the timed one
+      HIPCHECK(hipEventRecord(e0));
+      for (int i = 0; i < 200; i++) {
+        if (which == 0)
+          hipLaunchKernelGGL((k_parts<T>), dim3((nrows + 3) / 4), dim3(256), 0, 0, d_part, d_s,
+                             nrows, ppr, 0u, d_st, d_scur, d_v, 0u, nullptr, 0u, 0u, 0u, d_inv);
+        else
+          hipLaunchKernelGGL((k_parts_seg<T, 16>), dim3((nrows + 15) / 16), dim3(256), 0, 0,
+                             d_part, d_s, nrows, ppr, 0u, d_st, d_scur, d_v, 0u, d_inv);
+      }
+      HIPCHECK(hipEventRecord(e1));
+      HIPCHECK(hipEventSynchronize(e1));
+      HIPCHECK(hipEventElapsedTime(&ms[which], e0, e1));
+    }
+  }
+  std::printf("timing %u rows x %u partials: k_parts %.2f us, k_parts_seg %.2f us per launch "
+              "(back to back)\n", nrows, ppr, ms[0] * 5.0f, ms[1] * 5.0f);
+  HIPCHECK(hipFree(d_part));
+  HIPCHECK(hipFree(d_s));
+  HIPCHECK(hipFree(d_inv));
+  HIPCHECK(hipFree(d_scur));
+  HIPCHECK(hipFree(d_v));
+  HIPCHECK(hipFree(d_st));
+  return 0;
+}
+
 int
 main()
 {
+  time_case<double>(8192, 8);
+  time_case<double>(5824, 12);
   int bad = 0, cases = 0;
   for (uint32_t ppr = 1; ppr <= 32; ppr++)
     for (uint32_t nrows : { 1u, 3u, 17u, 1003u, 8192u }) {

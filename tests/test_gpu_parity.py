@@ -1075,7 +1075,7 @@ def test_single_launch_dropin_is_one_launch(eigen, orc):
 @pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float32, 6144),
                                   (np.float64, 8192),    # configs[1]: 1-row tiles of 8
                                   (np.float64, 4353),    # odd: element-wide access
-                                  # just past 2 GiB: non-temporal, 4 rounds per
+                                  # just past 2 GiB: non-temporal, 6 rounds per
                                   # store, element-wide (n % 16 B != 0)
                                   (np.float64, 16385), (np.float32, 23171)])
 @pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
@@ -1094,6 +1094,38 @@ def test_deferred_writes_bitwise(solver, dt, n, sem):
                (r2[0], r2[2], r2[3]["rounds"], r2[3]["converged"]), kw
         assert torch.equal(r1[1], r2[1]), kw                # v bitwise
         assert torch.equal(a1, a2), kw                      # final matrix bitwise
+
+
+@pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float64, 16385),
+                                  (np.float32, 6144), (np.float32, 23171)])
+def test_deferred_caps_do_not_change_results(solver, dt, n):
+    """The workgroups-per-CU caps of the deferred launches (st_set_defer_caps,
+    dynamic LDS reserved per workgroup) change residency only: a solve under
+    the shipped table, with every cap removed and with every slot at 2 / 8
+    per CU is bit-identical (λ, v, iterations, final matrix)."""
+    L = _lib.load()
+    d = 1 if dt == np.float64 else 0
+    nt = 1 if n * n * np.dtype(dt).itemsize >= (2 << 30) else 0
+    base = dev.generate("random", n, TD[dt], seed=8, device=DEV)
+    slots = (0, 1, 2, 3, 4, 6)
+    saved = {sl: L.st_set_defer_caps(d, nt, sl, 0) for sl in slots}     # read + clear
+    try:
+        for sl in slots:
+            L.st_set_defer_caps(d, nt, sl, saved[sl])                   # shipped table
+        out = []
+        for cap in (None, 0, 2, 8):
+            if cap is not None:
+                for sl in slots:
+                    assert L.st_set_defer_caps(d, nt, sl, cap) >= 0
+            a = base.clone()
+            r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
+            out.append((r[0], r[2], r[1].cpu(), a))
+        for o in out[1:]:
+            assert o[0] == out[0][0] and o[1] == out[0][1]
+            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
+    finally:
+        for sl in slots:
+            L.st_set_defer_caps(d, nt, sl, saved[sl])
 
 
 @pytest.mark.parametrize("limit", [8, 1000, 4096])
