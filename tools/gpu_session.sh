@@ -90,6 +90,13 @@ for s in $STEPS; do
       step capsab2_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 5 --caps-ab "$NT_SPECS" --ab-json "$OUT/${RTAG}_capsab2_random65536_p8_f64.json"
       step capsab2_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 5 --caps-ab "$F32_SPECS" --ab-json "$OUT/${RTAG}_capsab2_random32768_f32.json"
       step capsab2_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab2_hilbert8192_f64.json" ;;
+    capsab3) # cached blocks: the NP = 0 (post-store) and storing slots
+      C_SPECS="0,4,4,3,3,0,3;8,4,4,3,3,0,3;6,4,4,3,3,0,3;0,4,4,3,3,0,2;0,4,4,3,3,0,4;0,3,3,3,3,0,3"
+      F32C_SPECS="0,0,0,0,0,0,0;0,0,0,0,0,0,3;0,0,0,0,0,0,4;0,0,0,0,4,0,0;8,0,0,0,0,0,0"
+      step capsab3_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 7 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_hilbert8192_f64.json"
+      step capsab3_f64_6144 300 python3 tools/defer_profile.py --kind random --n 6144 --dtype f64 --cycles 60 --passes 7 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_random6144_f64.json"
+      step capsab3_f64_p8w 300 python3 tools/defer_profile.py --kind hilbert --n 23040 --rank-block 8 --dtype f64 --cycles 40 --passes 7 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_hilbert23040_p8_f64.json"
+      step capsab3_f32_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f32 --cycles 60 --passes 7 --caps-ab "$F32C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_hilbert8192_f32.json" ;;
     sq) # SQ instruction / wait counters of the deferred launches (two PMC passes)
       C1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
       C2="SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"
