@@ -966,7 +966,7 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool FULL = false>
+          int DS = -1>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -1000,9 +1000,6 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
   // compile time (1 / 0; the library's launches), or -1 = pend.store at
   // run time (the sweep tools)
-  // FULL: every row group has its R rows and every piece its PWC columns
-  // (nrows % R == 0, ncols % PWC == 0; the launcher checks): no row or
-  // column predicates at all
   if constexpr (GATE != kGateSpec) {
     if (flat_gated<GATE>(state, k))
       return;
@@ -1075,7 +1072,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
   for (int u = 0; u < U; u++) {
     const uint32_t c = c0 + u * BLK * W;
-    in_cols[u] = FULL || c < ncols;
+    in_cols[u] = c < ncols;
     in[u] = in_cols[u] && (SPLIT == 0 || ((c >= col0 && c < col1) == (SPLIT == 1)));
   }
   // SPLIT == 0 loads without predicates: a row past the block reads the
@@ -1105,12 +1102,12 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
       for (int u = 0; u < U; u++)
         x[u][j] = ld<V, NT>(reinterpret_cast<const V*>(ap + cl[u]));
-      if (FULL || r0 + j + 1 < nrows) // uniform
+      if (r0 + j + 1 < nrows) // uniform
         ap += ncols;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++)
-        if (in[u] && (FULL || r0 + j < nrows))
+        if (in[u] && r0 + j < nrows)
           x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
                                                    u * BLK * W));
     }
@@ -1148,7 +1145,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // fp64 with its store decision fixed at compile time too,
   // profiles/r03_store_probe_caps_nt.log "DS=1")
   constexpr bool kMergeRows = sizeof(T) == 8 && NP >= 1 && NP <= 4;
-  if (kMergeRows && (FULL || r0 + R <= nrows)) { // uniform
+  if (kMergeRows && r0 + R <= nrows) { // uniform
 #pragma unroll
     for (int j = 0; j < R; j++)
       sr[j] = ld_row(rs + row0 + r0 + j);
@@ -1163,13 +1160,13 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   } else {
 #pragma unroll
     for (int j = 0; j < R; j++)
-      sr[j] = (FULL || r0 + j < nrows) ? ld_row(rs + row0 + r0 + j) : (T)1;
+      sr[j] = r0 + j < nrows ? ld_row(rs + row0 + r0 + j) : (T)1;
     if constexpr (NP > 0) {
 #pragma unroll
       for (int i = 0; i < NP; i++) {
 #pragma unroll
         for (int j = 0; j < R; j++)
-          sp_r[i][j] = (FULL || r0 + j < nrows) ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
+          sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
       }
     }
   }
@@ -1227,7 +1224,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         y = x[u][j] * (inv * sc[u]); // cpp:324-325
       else
         y = (inv * x[u][j]) * sc[u]; // main.py:13-16
-      if (do_store && in_cols[u] && (FULL || r0 + j < nrows))
+      if (do_store && in_cols[u] && r0 + j < nrows)
         st<V, NTS>(reinterpret_cast<V*>(wp), y);
       wp += ncols;
       const T h = in_cols[u] ? hsum<T, W>(y) : (T)0;
@@ -1244,7 +1241,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       for (int i = 0; i < NP; i++) {
 #pragma unroll
         for (int j = 0; j < R; j++) {
-          if (FULL || r0 + j < nrows) {
+          if (r0 + j < nrows) {
             const T inv = sp_r[i][j];
             if constexpr (ORDER == 0)
               x[u][j] = x[u][j] * (inv * sp_c[i][u]);
@@ -1256,7 +1253,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     }
 #pragma unroll
     for (int j = 0; j < R; j++) {
-      if (FULL || r0 + j < nrows) {
+      if (r0 + j < nrows) {
         const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
@@ -1270,7 +1267,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       }
     }
   }
-  if (!FS && SPLIT == 0 && p == 0 && threadIdx.x < R && (FULL || r0 + threadIdx.x < nrows)) {
+  if (!FS && SPLIT == 0 && p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
     // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats
     const uint32_t r = row0 + r0 + threadIdx.x;
     const T m = (T)state->max;
@@ -1305,7 +1302,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
   if constexpr (!PW) {
     __syncthreads();
-    if (threadIdx.x < R && (FULL || r0 + threadIdx.x < nrows)) {
+    if (threadIdx.x < R && r0 + threadIdx.x < nrows) {
       T t = red[0][threadIdx.x];
 #pragma unroll
       for (int w = 1; w < NW; w++)

@@ -302,7 +302,7 @@ report(const Block& b, const char* what, float ms, bool store)
 // the library's launch: k_flat fp64 (non-temporal, 4 KB pieces, or cached,
 // 8 KB pieces), FS stats, ALT, NP pending; `lds` bytes of dynamic LDS per
 // workgroup cap the workgroups per CU
-template <int R, int NP, bool NT = true, int DS = -1, bool FULL = false>
+template <int R, int NP, bool NT = true, int DS = -1>
 static void
 lib_launch(const Block& b, int k, unsigned pt, bool store, unsigned lds = 0)
 {
@@ -319,7 +319,7 @@ lib_launch(const Block& b, int k, unsigned pt, bool store, unsigned lds = 0)
   const unsigned ppr = b.n / (256 * W * U);
   const unsigned grid = b.nr / R * ppr;
   hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, NPK, U, false,
-                             DS, FULL>),
+                             DS>),
                      dim3(grid), dim3(256), lds, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, ppr,
                      0u, (uint32_t)k, b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pd);
 }
@@ -351,29 +351,6 @@ cap_sweep(const Block& b)
       report(b, w, ms, store);
     }
   };
-  if (NT && std::getenv("SP_FULL")) { // the predicate-free (FULL) k_flat against the shipped one
-    const unsigned fc[] = { 0, 3 };
-    auto two = [&](const char* what, auto a, auto f, bool store) {
-      for (unsigned c : fc) {
-        for (int rep = 0; rep < 2; rep++) {
-          char w[96];
-          std::snprintf(w, sizeof w, "%s cap=%u", what, c);
-          report(b, w, time_seq([&](int k) { a(k, lds_for(c)); }), store);
-          std::snprintf(w, sizeof w, "%s cap=%u FULL", what, c);
-          report(b, w, time_seq([&](int k) { f(k, lds_for(c)); }), store);
-        }
-      }
-    };
-    two("every R=2 PT=4", [&](int k, unsigned l) { lib_launch<2, -1, NT>(b, k, 4, true, l); },
-        [&](int k, unsigned l) { lib_launch<2, -1, NT, -1, true>(b, k, 4, true, l); }, true);
-    two("NP=0 R=2 PT=8", [&](int k, unsigned l) { lib_launch<2, 0, NT, 0>(b, k, 8, false, l); },
-        [&](int k, unsigned l) { lib_launch<2, 0, NT, 0, true>(b, k, 8, false, l); }, false);
-    two("NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, NT, 0>(b, k, 16, false, l); },
-        [&](int k, unsigned l) { lib_launch<8, 4, NT, 0, true>(b, k, 16, false, l); }, false);
-    two("store NP=5 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 5, NT, 1>(b, k, 0, true, l); },
-        [&](int k, unsigned l) { lib_launch<8, 5, NT, 1, true>(b, k, 0, true, l); }, true);
-    return;
-  }
   if (NT) {
     one("every R=2 PT=4", [&](int k, unsigned l) { lib_launch<2, -1, NT>(b, k, 4, true, l); }, true);
     one("NP=0 R=2 PT=8", [&](int k, unsigned l) { lib_launch<2, 0, NT>(b, k, 8, false, l); }, false);
