@@ -144,6 +144,9 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"st_epilogue_{sfx}").argtypes = [P, P, u32, T, u32, u32, P, P]
         getattr(L, f"st_round_{sfx}").argtypes = [P, P, P, P, u32, u32, u32, T, u32, u32,
                                                   u32, P, P]
+        getattr(L, f"st_mfree_round_flat_{sfx}").argtypes = [P, P, P, P, P, P, u32, u32, u32,
+                                                              T, u32, u32, u32, P, P]
+        getattr(L, f"st_mfree_round_flat_{sfx}").restype = i32
         getattr(L, f"st_mfree_round_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, T, u32,
                                                         u32, u32, P, P]
         getattr(L, f"st_round_split_{sfx}").argtypes = [P, P, P, P, P, u32, u32, u32, u32,

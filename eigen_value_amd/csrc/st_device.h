@@ -966,7 +966,7 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1>
+          int DS = -1, bool MF = false>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -1000,8 +1000,16 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
   // compile time (1 / 0; the library's launches), or -1 = pend.store at
   // run time (the sweep tools)
+  // MF: the matrix-free round's sweep (launch k >= 1 of k_mfree's scheme,
+  // with FS): `a` is A_0 (read only), `v` is v_{k-2}; each piece's partial
+  // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
+  // group folds round k-1's stats, nothing is stored; k_mparts finishes
+  // s_k and v_{k-1}
+  static_assert(!MF || (FS && NP < 0 && SPLIT == 0), "MF: the fused-stats unsplit round");
+  // the matrix-free launch k evaluates round k - 1 (gated once end <= k - 1)
+  const uint32_t kr = MF ? k - 1 : k;
   if constexpr (GATE != kGateSpec) {
-    if (flat_gated<GATE>(state, k))
+    if (flat_gated<GATE>(state, kr))
       return;
   }
   using V = typename vec<T, W>::type;
@@ -1119,6 +1127,14 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   for (int u = 0; u < U; u++)
     if (UM || in_cols[u])
       sc[u] = *reinterpret_cast<const V*>(s_cur + cl[u]);
+  // matrix-free: x = v_{k-2} ∘ s_{k-1} for the piece's columns
+  V xs[MF ? U : 1];
+  if constexpr (MF) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (in_cols[u])
+        xs[u] = *reinterpret_cast<const V*>(v + cl[u]) * sc[u];
+  }
   // deferred writes: the pending rounds' column scales
   V sp_c[NP > 0 ? NP : 1][U];
   T sp_r[NP > 0 ? NP : 1][R]; // 1 / s_i[r]
@@ -1194,7 +1210,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
         for (int w = 1; w < NW; w++)
           m = mx_sh[w] > m ? mx_sh[w] : m;
-        stats_publish<T>(m, fail, ppr, s_cur, k, max_itr, semantics, state);
+        stats_publish<T>(m, fail, ppr, s_cur, kr, max_itr, semantics, state);
       }
     }
   }
@@ -1254,6 +1270,17 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
     for (int j = 0; j < R; j++) {
       if (r0 + j < nrows) {
+        if constexpr (MF) {
+          // A_0[r][c] x[c], fused, the lane's columns in order
+          if constexpr (W == 1) {
+            acc[j] = __builtin_fma(x[u][j], xs[u], acc[j]);
+          } else {
+#pragma unroll
+            for (int i = 0; i < W; i++)
+              acc[j] = __builtin_fma(x[u][j][i], xs[u][i], acc[j]);
+          }
+          continue;
+        }
         const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
@@ -1377,6 +1404,42 @@ k_parts_t(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
     const T m = (T)state->max;
     v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
   }
+}
+
+// The matrix-free round's second launch (after k_flat<..., MF>): one wave
+// per row sums its pieces in k_parts' order, s_k[r] = Σ / x[r] with
+// x[r] = v_{k-2}[r] s_{k-1}[r] (k_mfree's quotient); the blocks past the
+// rows write v_{k-1} = v_{k-2} ∘ (s_{k-1} / m_{k-1}) over ALL n entries
+// (every rank of a sharded solve keeps the whole v), m_{k-1} as k_flat's
+// first row group published it.  Gated like launch k (end < k).
+template <typename T, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_mparts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
+         uint32_t ppr, uint32_t k, const st_state* state, const T* __restrict__ s_prev,
+         const T* __restrict__ v_prev, T* __restrict__ v_cur, uint32_t row0, uint32_t n,
+         uint32_t row_blocks)
+{
+  const uint32_t e = state->end; // plain load: as k_parts
+  if (e != 0 && e < k)
+    return;
+  if (blockIdx.x >= row_blocks) {
+    const T m = (T)state->max;
+    const uint32_t nb = gridDim.x - row_blocks;
+    for (uint32_t i = (blockIdx.x - row_blocks) * BLK + threadIdx.x; i < n; i += nb * BLK)
+      v_cur[i] = v_prev[i] * (s_prev[i] / m); // cpp:260
+    return;
+  }
+  const uint32_t r = (blockIdx.x * BLK + threadIdx.x) >> 6;
+  const uint32_t lane = threadIdx.x & 63;
+  if (r >= nrows)
+    return; // whole waves leave together
+  const T* row = part + (size_t)r * ppr;
+  T acc = (T)0;
+  for (uint32_t p = lane; p < ppr; p += 64)
+    acc += row[p];
+  acc = wave_sum(acc);
+  if (lane == 0)
+    s_next[r] = acc / (v_prev[row0 + r] * s_prev[row0 + r]);
 }
 
 // k_parts for rows of at most LPR (16 or 32) partials: 64 / LPR rows per

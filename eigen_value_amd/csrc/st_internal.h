@@ -97,6 +97,13 @@ int launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
                  T* v_cur, uint32_t nrows, uint32_t ncols, uint32_t row0,
                  T eps, uint32_t k, uint32_t max_itr, uint32_t semantics,
                  st_state* st, hipStream_t stream);
+// the matrix-free round in the flat form (k_flat<MF> + k_mparts); `part`
+// holds round_flat_scratch(nrows, ncols) elements
+template <typename T>
+int launch_mfree_flat(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
+                      T* v_cur, T* part, uint32_t nrows, uint32_t ncols,
+                      uint32_t row0, T eps, uint32_t k, uint32_t max_itr,
+                      uint32_t semantics, st_state* st, hipStream_t stream);
 template <typename T>
 int launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
                     uint32_t semantics, st_state* st, hipStream_t stream);

@@ -522,6 +522,80 @@ launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
   return check_launch("mfree");
 }
 
+// ---- the matrix-free round, flat -------------------------------------------
+// k_flat<..., MF> over one 4 / 8 KB piece of R rows per workgroup (the
+// shapes of the deferred rounds' read-only NP = 0 launch: 2 rows in tiles of
+// 8 row groups on non-temporal blocks, 1 row in tiles of 4 on cached fp64
+// ones, 2 rows row-major on cached fp32 ones), the first row group folding
+// round k-1's stats, then k_mparts (s_k of the rows, v_{k-1} of all n).
+// Same row sums up to association as k_mfree (pieces summed apart).
+template <typename T, int W, bool NT>
+void
+launch_mfree_flat_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev, T* v_cur,
+                      T* part, uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+                      uint32_t k, uint32_t max_itr, uint32_t semantics, st_state* st,
+                      hipStream_t stream)
+{
+  constexpr int U = kFlatU<T, W, NT>;
+  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  constexpr int R = NT ? 2 : kF64C ? 1 : 2;
+  const uint32_t ppr = flat_pieces(ncols, W * U);
+  const FlatGrid fg = flat_grid((nrows + R - 1) / R * ppr);
+  dev::FlatPending<T, -1> pe{};
+  pe.pt = NT ? 8u : kF64C ? 4u : 0u;
+  hipLaunchKernelGGL((dev::k_flat<T, W, 0, NT, R, false, true, kFlatAlt, kBlock, 0,
+                                  dev::kGatePlain, -1, U, false, -1, true>),
+                     fg.grid, dim3(kBlock), 0, stream, const_cast<T*>(a0), s_prev, part,
+                     const_cast<T*>(v_prev), nrows, ncols, ppr, row0, k, st, eps, max_itr,
+                     semantics, 0u, 0u, 0u, pe, fg.gx2);
+  const uint32_t rb = (nrows + dev::kWaves - 1) / dev::kWaves;
+  const uint32_t vb = (ncols + kBlock - 1) / kBlock < 256u ? (ncols + kBlock - 1) / kBlock
+                                                            : 256u;
+  hipLaunchKernelGGL((dev::k_mparts<T>), dim3(rb + vb), dim3(kBlock), 0, stream, part,
+                     s_next, nrows, ppr, k, st, s_prev, v_prev, v_cur, row0, ncols, rb);
+}
+
+template <typename T>
+int
+launch_mfree_flat(const T* a0, const T* s_prev, T* s_next, const T* v_prev, T* v_cur,
+                  T* part, uint32_t nrows, uint32_t ncols, uint32_t row0, T eps,
+                  uint32_t k, uint32_t max_itr, uint32_t semantics, st_state* st,
+                  hipStream_t stream)
+{
+  ST_REQUIRE(a0 && s_prev && s_next && v_prev && v_cur && part && st,
+             "mfree_flat: null pointer");
+  ST_REQUIRE(nrows > 0 && ncols > 0 && row0 + (uint64_t)nrows <= ncols,
+             "mfree_flat: bad block");
+  ST_REQUIRE(semantics <= ST_SEM_MAINPY, "mfree_flat: bad semantics %u", semantics);
+  ST_REQUIRE(k >= 1 && max_itr > 0, "mfree_flat: launch index k must be >= 1");
+  ST_REQUIRE(v_prev != v_cur, "mfree_flat: v_prev and v_cur must differ");
+  ST_REQUIRE((uint64_t)((nrows + kFlatRows - 1) / kFlatRows) * flat_pieces(ncols, 1) <
+               (1ull << 31),
+             "mfree_flat: %u x %u is too large for one launch", nrows, ncols);
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && aligned16(a0) && aligned16(s_prev) &&
+                      aligned16(v_prev);
+  const bool nt = flat_round_nt(nrows, ncols, sizeof(T));
+#define ST_MFF(WW, NN)                                                         \
+  launch_mfree_flat_cfg<T, WW, NN>(a0, s_prev, s_next, v_prev, v_cur, part, nrows, \
+                                   ncols, row0, eps, k, max_itr, semantics, st,   \
+                                   stream)
+  if (vec_ok)
+    nt ? ST_MFF(W, true) : ST_MFF(W, false);
+  else
+    nt ? ST_MFF(1, true) : ST_MFF(1, false);
+#undef ST_MFF
+  return check_launch("mfree_flat");
+}
+
+template int launch_mfree_flat<float>(const float*, const float*, float*, const float*,
+                                      float*, float*, uint32_t, uint32_t, uint32_t, float,
+                                      uint32_t, uint32_t, uint32_t, st_state*, hipStream_t);
+template int launch_mfree_flat<double>(const double*, const double*, double*, const double*,
+                                       double*, double*, uint32_t, uint32_t, uint32_t,
+                                       double, uint32_t, uint32_t, uint32_t, st_state*,
+                                       hipStream_t);
+
 template <typename T>
 int
 launch_round(T* a, const T* s_cur, T* s_next, T* v, uint32_t nrows,
@@ -1396,6 +1470,20 @@ st_state_reset(st_state* d_state, void* stream)
     return st::launch_mfree<T>(d_mat0, d_s_prev, d_s_next, d_v_prev, d_v_cur,  \
                                nrows, ncols, row0, eps, k, max_itr, semantics, \
                                d_state, ST_STREAM(stream));                    \
+  }                                                                            \
+  int st_mfree_round_flat_##SFX(const T* d_mat0, const T* d_s_prev,            \
+                                T* d_s_next, const T* d_v_prev, T* d_v_cur,    \
+                                T* d_part, unsigned int nrows,                 \
+                                unsigned int ncols, unsigned int row0, T eps,  \
+                                unsigned int k, unsigned int max_itr,          \
+                                unsigned int semantics, st_state* d_state,     \
+                                void* stream)                                  \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_mfree_flat<T>(d_mat0, d_s_prev, d_s_next, d_v_prev,      \
+                                    d_v_cur, d_part, nrows, ncols, row0, eps,  \
+                                    k, max_itr, semantics, d_state,            \
+                                    ST_STREAM(stream));                        \
   }                                                                            \
   int st_epilogue_##SFX(const T* d_s, T* d_v, unsigned int n, T eps,           \
                         unsigned int max_itr, unsigned int semantics,          \

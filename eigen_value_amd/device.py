@@ -156,6 +156,24 @@ def mfree_round(mat0, s_prev, s_next, v_prev, v_cur, state, row0: int = 0,
         row0, eps, k, max_itr, semantics, _ptr(state), _stream(mat0.device)), "mfree_round")
 
 
+def mfree_round_flat(mat0, s_prev, s_next, v_prev, v_cur, part, state, row0: int = 0,
+                     eps: float = 1e-3, k: int = 1, max_itr: int = _lib.ST_MAX_ITR,
+                     semantics: int = _lib.ST_SEM_SYCL) -> None:
+    """mfree_round in the flat form (``st_mfree_round_flat_*``): partial dot
+    products per 4 / 8 KB piece into ``part`` (flat_scratch), then s_k and
+    v_{k-1}; the solve loops' form for blocks where flat_round_pays."""
+    _check_cuda(mat0, s_prev, s_next, v_prev, v_cur, part, state)
+    assert mat0.is_contiguous() and mat0.dim() == 2
+    nrows, ncols = mat0.shape
+    assert s_prev.numel() >= ncols and v_prev.numel() >= ncols and v_cur.numel() >= ncols
+    assert s_next.numel() >= nrows and row0 + nrows <= ncols
+    assert part.numel() >= int(_lib.load().st_round_flat_scratch(nrows, ncols))
+    _lib.check(getattr(_lib.load(), f"st_mfree_round_flat_{_sfx(mat0)}")(
+        _ptr(mat0), _ptr(s_prev), _ptr(s_next), _ptr(v_prev), _ptr(v_cur), _ptr(part), nrows,
+        ncols, row0, eps, k, max_itr, semantics, _ptr(state), _stream(mat0.device)),
+        "mfree_round_flat")
+
+
 def flat_round_pays(nrows: int, ncols: int, dtype) -> bool:
     """Whether the flat round (st_round_flat) is the faster form for a block."""
     torch = _torch()

@@ -463,6 +463,27 @@ int st_mfree_round_f64(const double* d_mat0, const double* d_s_prev,
                        unsigned int row0, double eps, unsigned int k,
                        unsigned int max_itr, unsigned int semantics,
                        st_state* d_state, void* stream);
+/* The same matrix-free launch k in the flat form (the solve loops' choice
+ * for blocks where st_round_flat_pays): one short workgroup per (rows, 4 or
+ * 8 KB column piece) writes partial dot products into d_part
+ * (st_round_flat_scratch(nrows, ncols) elements), a second launch sums them
+ * per row and writes v_{k-1}.  Results equal st_mfree_round_* up to the
+ * association of the row sums (pieces summed apart; deterministic and
+ * independent of the row partition). */
+int st_mfree_round_flat_f32(const float* d_mat0, const float* d_s_prev,
+                            float* d_s_next, const float* d_v_prev,
+                            float* d_v_cur, float* d_part, unsigned int nrows,
+                            unsigned int ncols, unsigned int row0, float eps,
+                            unsigned int k, unsigned int max_itr,
+                            unsigned int semantics, st_state* d_state,
+                            void* stream);
+int st_mfree_round_flat_f64(const double* d_mat0, const double* d_s_prev,
+                            double* d_s_next, const double* d_v_prev,
+                            double* d_v_cur, double* d_part, unsigned int nrows,
+                            unsigned int ncols, unsigned int row0, double eps,
+                            unsigned int k, unsigned int max_itr,
+                            unsigned int semantics, st_state* d_state,
+                            void* stream);
 
 /* Round epilogue on the full row-sum vector s[0..n): m = max(0, max s)
  * (find_max, similarity_transform.cpp:154-227), v[i] *= s[i]/m
