@@ -405,6 +405,61 @@ sp_time(const Block& b, unsigned pt)
 
 static std::vector<unsigned> g_pts = { 0, 4, 16 };
 
+// the matrix-free round in the flat form (k_flat<..., MF> + k_mparts) by
+// rows per workgroup and piece tile, against k_mfree (the library's shape:
+// 4 rows, 2 chunks, 512 workgroups, non-temporal on >= 512 MiB); v_prev =
+// b.v, v_cur = b.inv[6], s_next = b.s[6]
+template <int R, bool NT>
+static void
+mf_launch(const Block& b, int k, unsigned pt, unsigned lds)
+{
+  constexpr int U = NT ? 1 : 2;
+  FlatPending<T, -1> pe{};
+  pe.pt = pt;
+  const unsigned ppr = b.n / (256 * W * U);
+  const unsigned grid = b.nr / R * ppr;
+  hipLaunchKernelGGL((k_flat<T, W, 0, NT, R, false, true, 2, 256, 0, kGatePlain, -1, U, false,
+                             -1, true>),
+                     dim3(grid), dim3(256), lds, 0, b.a, b.s[0], b.part, b.v, b.nr, b.n, ppr,
+                     0u, (uint32_t)(k + 1), b.st, (T)0, 1u << 30, 0u, 0u, 0u, 0u, pe);
+  const unsigned rb = (b.nr + 3) / 4, vb = std::min(256u, (b.n + 255) / 256);
+  hipLaunchKernelGGL((k_mparts<T>), dim3(rb + vb), dim3(256), 0, 0, b.part, b.s[6], b.nr, ppr,
+                     (uint32_t)(k + 1), b.st, b.s[0], b.v, b.inv[6], 0u, b.n, rb);
+}
+
+template <bool NT>
+static void
+mf_sweep(const Block& b)
+{
+  {
+    std::vector<T> ones(b.n, (T)1);
+    (void)hipMemcpy(b.v, ones.data(), sizeof(T) * b.n, hipMemcpyHostToDevice);
+  }
+  const unsigned ng = b.nr / 4;
+  report(b, "k_mfree R=4 (library shape)", time_seq([&](int k) {
+           hipLaunchKernelGGL((k_mfree<T, 4, W, 2, NT, 256, true>), dim3(std::min(512u, ng)),
+                              dim3(256), 0, 0, b.a, b.s[0], b.s[6], b.v, b.inv[6], ng, 0u, b.n,
+                              0u, (T)0, (uint32_t)(k + 1), 1u << 30, 0u, b.st);
+         }), false);
+  for (unsigned cap : { 0u, 5u, 4u }) {
+    for (unsigned pt : { 0u, 8u, 16u, 32u }) {
+      char w[96];
+      std::snprintf(w, sizeof w, "MF R=2 PT=%u cap=%u", pt, cap);
+      report(b, w, time_seq([&](int k) { mf_launch<2, NT>(b, k, pt, lds_for(cap)); }), false);
+      std::snprintf(w, sizeof w, "MF R=4 PT=%u cap=%u", pt, cap);
+      report(b, w, time_seq([&](int k) { mf_launch<4, NT>(b, k, pt, lds_for(cap)); }), false);
+      std::snprintf(w, sizeof w, "MF R=8 PT=%u cap=%u", pt, cap);
+      report(b, w, time_seq([&](int k) { mf_launch<8, NT>(b, k, pt, lds_for(cap)); }), false);
+      if (!NT) {
+        std::snprintf(w, sizeof w, "MF R=1 PT=%u cap=%u", pt, cap);
+        report(b, w, time_seq([&](int k) { mf_launch<1, NT>(b, k, pt, lds_for(cap)); }), false);
+      }
+    }
+  }
+}
+
+
+
 template <int RB, int NB, int NP, bool STORE>
 static void
 pipe_launch(const Block& b, int k, unsigned pt, unsigned lds)
@@ -505,7 +560,12 @@ run(unsigned nr, unsigned n, bool check)
     report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
            time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
   }
-  if (std::getenv("SP_PIPE")) { // the software-pipelined k_pipe against k_flat (capped)
+  if (std::getenv("SP_MF")) { // the flat matrix-free round's shapes
+    if (std::getenv("SP_CACHED"))
+      mf_sweep<false>(b);
+    else
+      mf_sweep<true>(b);
+  } else if (std::getenv("SP_PIPE")) { // the software-pipelined k_pipe against k_flat (capped)
     for (unsigned cap : { 0u, 4u, 3u }) {
       report(b, (std::string("k_flat store NP=5 R=8 PT=0 cap=") + std::to_string(cap)).c_str(),
              time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true, lds_for(cap)); }), true);
