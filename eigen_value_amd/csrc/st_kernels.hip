@@ -198,6 +198,14 @@ flat_round_pays(uint32_t nrows, uint32_t ncols, size_t elem)
   return block_bytes(nrows, ncols, elem) >= ((size_t)144 << 20);
 }
 
+// dynamic LDS that leaves room for `cap` workgroups per CU (160 KB of LDS
+// per CU on gfx950, k_flat's own few hundred bytes included)
+inline uint32_t
+defer_cap_lds(uint32_t cap)
+{
+  return cap < 2 ? 0u : (160u << 10) / cap - 2048u;
+}
+
 inline bool
 flat_round_nt(uint32_t nrows, uint32_t ncols, size_t elem)
 {
@@ -523,12 +531,17 @@ launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
 }
 
 // ---- the matrix-free round, flat -------------------------------------------
-// k_flat<..., MF> over one 4 / 8 KB piece of R rows per workgroup (the
-// shapes of the deferred rounds' read-only NP = 0 launch: 2 rows in tiles of
-// 8 row groups on non-temporal blocks, 1 row in tiles of 4 on cached fp64
-// ones, 2 rows row-major on cached fp32 ones), the first row group folding
-// round k-1's stats, then k_mparts (s_k of the rows, v_{k-1} of all n).
-// Same row sums up to association as k_mfree (pieces summed apart).
+// k_flat<..., MF> over one 4 / 8 KB piece of R rows per workgroup, the first
+// row group folding round k-1's stats, then k_mparts (s_k of the rows,
+// v_{k-1} of all n).  Same row sums up to association as k_mfree (pieces
+// summed apart).  Shapes (tools/store_probe SP_MF=1,
+// profiles/r03_mf_shapes_{nt,cached}.log; a flat launch + k_mparts against
+// one k_mfree launch): every lane's x = v ∘ s vector serves R rows, so 4 - 8
+// rows pay where the read-only deferred rounds take 1 - 2, and they want a
+// workgroup cap like the deferred rounds' (dynamic LDS): cached fp64 8 rows
+// in tiles of 8 row groups, 4 per CU (8192^2 0.0798 vs 0.0848 ms for
+// k_mfree); non-temporal 4 rows in tiles of 8, 5 per CU (32768^2 fp64 1.205
+// vs 1.216, 8192 x 65536 0.642 vs 0.644).
 template <typename T, int W, bool NT>
 void
 launch_mfree_flat_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev, T* v_cur,
@@ -537,15 +550,15 @@ launch_mfree_flat_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev, 
                       hipStream_t stream)
 {
   constexpr int U = kFlatU<T, W, NT>;
-  constexpr bool kF64C = !NT && sizeof(T) == 8;
-  constexpr int R = NT ? 2 : kF64C ? 1 : 2;
+  constexpr int R = NT ? 4 : 8;
   const uint32_t ppr = flat_pieces(ncols, W * U);
   const FlatGrid fg = flat_grid((nrows + R - 1) / R * ppr);
   dev::FlatPending<T, -1> pe{};
-  pe.pt = NT ? 8u : kF64C ? 4u : 0u;
+  pe.pt = 8u;
+  const uint32_t lds = defer_cap_lds(NT ? 5u : 4u);
   hipLaunchKernelGGL((dev::k_flat<T, W, 0, NT, R, false, true, kFlatAlt, kBlock, 0,
                                   dev::kGatePlain, -1, U, false, -1, true>),
-                     fg.grid, dim3(kBlock), 0, stream, const_cast<T*>(a0), s_prev, part,
+                     fg.grid, dim3(kBlock), lds, stream, const_cast<T*>(a0), s_prev, part,
                      const_cast<T*>(v_prev), nrows, ncols, ppr, row0, k, st, eps, max_itr,
                      semantics, 0u, 0u, 0u, pe, fg.gx2);
   const uint32_t rb = (nrows + dev::kWaves - 1) / dev::kWaves;
@@ -823,13 +836,6 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   { { 0, 4, 4, 3, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
-// dynamic LDS that leaves room for `cap` workgroups per CU (160 KB of LDS
-// per CU on gfx950, k_flat's own few hundred bytes included)
-inline uint32_t
-defer_cap_lds(uint32_t cap)
-{
-  return cap < 2 ? 0u : (160u << 10) / cap - 2048u;
-}
 
 template <typename T, bool NT>
 inline uint32_t
