@@ -712,6 +712,55 @@ def test_matrix_free_leaves_input_and_matches_transform(solver):
     assert it_x == 7 and st_x["rounds"] == 7 and st_x["converged"] == 0
 
 
+@pytest.mark.parametrize("dt,nr,n,row0", [(np.float64, 4352, 4352, 0),    # cached, 8 KB pieces
+                                          (np.float64, 2049, 6001, 3000),  # rank block, W = 1
+                                          (np.float32, 6144, 6144, 0),
+                                          (np.float64, 16385, 16385, 0)])  # 2 GiB: non-temporal
+def test_mfree_flat_form_matches_mfree(orc, dt, nr, n, row0):
+    """st_mfree_round_flat (k_flat<MF> + k_mparts, the flat form of the
+    matrix-free launch) against st_mfree_round over 9 launches from the same
+    block: the stats, λ, v and the row sums agree to the dtype's rounding
+    (the two sum a row in another association), the gated launch after a
+    stop is a no-op in both, and the flat form's sums do not depend on the
+    launch: two runs are bit-identical."""
+    tdt = TD[dt]
+    a = dev.generate("random", n, tdt, nrows=nr, row0=row0, seed=12, device=DEV)
+    part = dev.flat_scratch(nr, n, tdt, DEV)
+    s_full = torch.from_numpy(orc.random_matrix(n, 13, np.float64, nrows=1)[0] + 0.5).to(DEV)
+
+    def run(flat, eps=0.0, launches=9):
+        s = [s_full.to(tdt).clone(), s_full.to(tdt).clone()]
+        v = [torch.ones(n, dtype=tdt, device=DEV) for _ in range(2)]
+        st = dev.new_state(DEV)
+        dev.rowsum(a, out=s[0][row0:row0 + nr])
+        for k in range(1, launches + 1):
+            args = (a, s[(k - 1) & 1], s[k & 1][row0:row0 + nr], v[(k - 1) & 1], v[k & 1])
+            if flat:
+                dev.mfree_round_flat(*args, part, st, row0=row0, eps=eps, k=k, max_itr=1000)
+            else:
+                dev.mfree_round(*args, st, row0=row0, eps=eps, k=k, max_itr=1000)
+        torch.cuda.synchronize()
+        return s[launches & 1].clone(), v[launches & 1].clone(), dev.read_state(st)
+
+    tol = 1e-12 if dt == np.float64 else 2e-5
+    sf, vf, stf = run(True)
+    sk, vk, stk = run(False)
+    assert (stf["round"], stf["stop"], stf["done"]) == (stk["round"], stk["stop"], stk["done"])
+    assert abs(stf["eigen_val"] - stk["eigen_val"]) <= tol * abs(stk["eigen_val"])
+    assert abs(stf["max"] - stk["max"]) <= tol * abs(stk["max"])
+    assert ((vf - vk).abs() / vk.abs()).max().item() <= tol
+    rows = slice(row0, row0 + nr)
+    assert ((sf[rows] - sk[rows]).abs() / sk[rows].abs()).max().item() <= tol
+    sf2, vf2, _ = run(True)
+    assert torch.equal(sf, sf2) and torch.equal(vf, vf2)              # deterministic
+    # a huge eps stops at round 0: launch 1 records it, launches 2.. are gated
+    # (v_0 and s_1, in the odd buffers, stay as launch 1 left them)
+    sf3, vf3, st3 = run(True, eps=1e30, launches=5)
+    sk3, vk3, sk3st = run(False, eps=1e30, launches=5)
+    assert st3["done"] == sk3st["done"] == 1 and st3["end"] == sk3st["end"] == 1
+    assert ((vf3 - vk3).abs() / vk3.abs()).max().item() <= tol
+
+
 def _gpu_gloo_mfree_worker(rank, world, port, n, outdir):
     import torch.distributed as dist
     from eigen_value_amd.sharded import ShardedSimilarityTransform
