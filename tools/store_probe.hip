@@ -49,7 +49,7 @@ using V = vec<double, 2>::type;
 constexpr int W = 2;
 constexpr int BLK = 256;
 constexpr int NW = BLK / 64;
-constexpr int kRing = 7;
+constexpr int kRing = 9; // s_k and up to 7 pending + 1
 
 template <int NP>
 struct Pend
@@ -560,7 +560,31 @@ run(unsigned nr, unsigned n, bool check)
     report(b, "k_flat store NP=5 R=8 PT=0 (lib)",
            time_seq([&](int k) { lib_launch<8, 5>(b, k, 0, true); }), true);
   }
-  if (std::getenv("SP_MF")) { // the flat matrix-free round's shapes
+  if (std::getenv("SP_LONGM")) { // longer store cycles: the launches m = 7, 8 would add
+    const bool nt = !std::getenv("SP_CACHED");
+    auto row = [&](const char* what, auto launch, bool store) {
+      for (unsigned c : { 0u, 5u, 4u, 3u }) {
+        char w[96];
+        std::snprintf(w, sizeof w, "%s cap=%u", what, c);
+        report(b, w, time_seq([&](int k) { launch(k, lds_for(c)); }), store);
+      }
+    };
+    if (nt) {
+      row("read NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, true, 0>(b, k, 16, false, l); }, false);
+      row("read NP=5 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 5, true, 0>(b, k, 16, false, l); }, false);
+      row("read NP=6 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 6, true, 0>(b, k, 16, false, l); }, false);
+      row("store NP=5 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 5, true, 1>(b, k, 0, true, l); }, true);
+      row("store NP=6 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 6, true, 1>(b, k, 0, true, l); }, true);
+      row("store NP=7 R=8 PT=0", [&](int k, unsigned l) { lib_launch<8, 7, true, 1>(b, k, 0, true, l); }, true);
+    } else {
+      row("read NP=4 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 4, false, 0>(b, k, 16, false, l); }, false);
+      row("read NP=5 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 5, false, 0>(b, k, 16, false, l); }, false);
+      row("read NP=6 R=8 PT=16", [&](int k, unsigned l) { lib_launch<8, 6, false, 0>(b, k, 16, false, l); }, false);
+      row("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, false, 1>(b, k, 4, true, l); }, true);
+      row("store NP=6 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 6, false, 1>(b, k, 4, true, l); }, true);
+      row("store NP=7 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 7, false, 1>(b, k, 4, true, l); }, true);
+    }
+  } else if (std::getenv("SP_MF")) { // the flat matrix-free round's shapes
     if (std::getenv("SP_CACHED"))
       mf_sweep<false>(b);
     else
