@@ -68,3 +68,43 @@ def test_sweep_table(tmp_path):
     assert "1024x4096 32" in out and "2048 64" in out
     row = [ln for ln in out.splitlines() if ln.startswith("(4, 0, 1, 256)")][0]
     assert "2.000" in row
+
+
+def _kflat(np_, store):
+    # k_flat's template arguments as rocprofv3 prints them (NP is the 12th)
+    return ("void st::dev::k_flat<double, 2, 0, true, 8, false, true, 2, 256, 0, 1, "
+            f"{np_}, 1, false, {1 if store else 0}>(double*, double const*)")
+
+
+def test_defer_profile_cycle_and_launch_rows(tmp_path):
+    """tools/defer_profile.py summary mode: per-NP averages of k_flat and of
+    the k_parts launch that follows each, the cycle sum per round, and the
+    per-launch CSV (the trimmed trace the committed summaries cite) holding
+    exactly the deferred launches."""
+    m, n = 6, 1024
+    rows, t = [], 0
+    for cyc in range(2):
+        for np_ in range(m):
+            dur = 2000 if np_ == m - 1 else 1000
+            rows.append({"Kernel_Name": _kflat(np_, np_ == m - 1), "Start_Timestamp": t,
+                         "End_Timestamp": t + dur})
+            t += dur + 10
+            rows.append({"Kernel_Name": "void st::dev::k_parts_seg<double, 16, 256>(double const*)",
+                         "Start_Timestamp": t, "End_Timestamp": t + 100})
+            t += 110
+            rows.append({"Kernel_Name": "other_kernel", "Start_Timestamp": t,
+                         "End_Timestamp": t + 5})
+            t += 10
+    _write(tmp_path / "trace.csv", ["Kernel_Name", "Start_Timestamp", "End_Timestamp"], rows)
+    out, lc = tmp_path / "cycle.json", tmp_path / "cycle_launches.csv"
+    subprocess.run([sys.executable, os.path.join(TOOLS, "defer_profile.py"), "--n", str(n),
+                    "--trace", str(tmp_path / "trace.csv"), "--json", str(out),
+                    "--launches", str(lc)], check=True, capture_output=True)
+    d = json.load(open(out))
+    assert d["trace"] == "cycle_launches.csv" and d["m"] == m
+    assert d["k_flat"]["0"]["launches"] == 2 and d["k_flat"]["5"]["avg_ms"] == 0.002
+    assert d["cycle_ms_per_round"] == round((5 * 0.0011 + 0.0021) / 6, 5)     # rounded to 10 ns
+    launch_rows = list(csv.DictReader(open(lc)))
+    assert len(launch_rows) == 2 * m * 2                      # k_flat + k_parts, no others
+    assert {r["kernel"] for r in launch_rows} == {"k_flat", "k_parts"}
+    assert launch_rows[0]["start_ns"] == "0" and launch_rows[0]["np"] == "0"

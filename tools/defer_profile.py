@@ -129,7 +129,7 @@ def summarise(path, n, elem, m, workload, events=None, launches=None):
             last = np_of(name)
             flat.setdefault(last, []).append(dur(r))
             kept.append(("k_flat", last, r))
-        elif "k_parts<" in name and last is not None:
+        elif ("k_parts<" in name or "k_parts_seg<" in name) and last is not None:
             parts.setdefault(last, []).append(dur(r))
             kept.append(("k_parts", last, r))
             last = None

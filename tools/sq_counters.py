@@ -17,7 +17,7 @@ import sys
 
 
 def key(name):
-    if "k_parts<" in name:
+    if "k_parts<" in name or "k_parts_seg<" in name:
         return "k_parts"
     m = re.search(r"k_flat<([^>]*)>", name)
     if not m:
