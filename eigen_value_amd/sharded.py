@@ -184,12 +184,16 @@ class RcclComm:
         rank = dist.get_rank(group)
         dev = torch.cuda.current_device() if device_index is None else device_index
         uid = ctypes.create_string_buffer(128)
-        if rank == 0:
-            _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
-        obj = [uid.raw if rank == 0 else None]
+        # rank 0's failure to make an id reaches every rank (None is
+        # broadcast), so no rank is left waiting in ncclCommInitRank
+        obj = [None]
+        if rank == 0 and self.L.st_comm_unique_id(uid) == 0:
+            obj = [uid.raw]
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
                                    group=group)
         self.comm = ctypes.c_void_p()
+        if obj[0] is None:
+            raise _lib.EigenValueError("st_comm_unique_id failed on rank 0")
         _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, obj[0], dev),
                    "st_comm_init")
         self.rank, self.world = rank, world
@@ -212,6 +216,29 @@ class RcclComm:
         if self.comm is not None and self.comm.value:
             self.L.st_comm_destroy(self.comm)
             self.comm = self.ctypes.c_void_p()
+
+
+def make_comm_agreed(group, factory, device=None):
+    """factory() on every rank of `group`, then one all-reduce (MIN) of
+    whether it succeeded: a communicator is used only if EVERY rank has one
+    - otherwise all ranks close theirs and return (None, reason), so no rank
+    issues the library all-gather while another waits in torch's (a mixed
+    exchange would hang the first round)."""
+    import torch
+    import torch.distributed as dist
+    comm, err = None, None
+    try:
+        comm = factory()
+    except Exception as e:  # noqa: BLE001 - agreed on below
+        err = f"{type(e).__name__}: {e}"
+    flag = torch.tensor([0 if comm is None else 1], dtype=torch.int32,
+                        device=device if device is not None else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
+    if int(flag.item()) == 1:
+        return comm, None
+    if comm is not None:
+        comm.close()
+    return None, err or "another rank could not create its communicator"
 
 
 def _allgather(out, inp, group=None):
@@ -286,13 +313,14 @@ class ShardedSimilarityTransform:
         if world > 1 and not self.rehearsal and comm != "torch" \
                 and isinstance(self.ops, HipShardOps) \
                 and dist.get_backend(group) == "nccl":
-            try:
-                self.rccl = RcclComm(group)
-            except Exception as e:          # auto: keep torch's RCCL group
+            self.rccl, err = make_comm_agreed(group, lambda: RcclComm(group),
+                                              device=torch.device(
+                                                  "cuda", torch.cuda.current_device()))
+            if self.rccl is None:           # auto: every rank keeps torch's RCCL group
                 if comm == "native":
-                    raise
+                    raise _lib.EigenValueError(f"library RCCL communicator: {err}")
                 import warnings
-                warnings.warn(f"library RCCL communicator unavailable ({e}); "
+                warnings.warn(f"library RCCL communicator unavailable ({err}); "
                               "using torch.distributed all_gather_into_tensor")
 
     def _vec(self):

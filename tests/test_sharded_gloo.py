@@ -543,3 +543,44 @@ def test_world8_sharded_solve_vs_oracle(world8_runs, orc, case):
             kinds.add((bool(deferred), int(m)))
     if mode == "defer":
         assert kinds == {(False, 0), (True, 2), (True, 3), (True, 4)}
+
+
+class _FakeComm:
+    closed = 0
+
+    def close(self):
+        _FakeComm.closed += 1
+
+
+def _agree_worker(rank, world, port, fail_rank, outdir):
+    from eigen_value_amd.sharded import make_comm_agreed
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def factory():
+            if rank == fail_rank:
+                raise RuntimeError("no RCCL here")
+            return _FakeComm()
+        comm, err = make_comm_agreed(None, factory)
+        np.save(os.path.join(outdir, f"agree{rank}.npy"),
+                np.array([comm is not None, _FakeComm.closed, err is not None]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [-1, 0, 2])
+def test_library_comm_is_used_only_if_every_rank_has_one(tmp_path, fail_rank):
+    """sharded.make_comm_agreed (how ShardedSimilarityTransform takes the
+    library's RCCL communicator on an nccl group): one rank failing to create
+    it makes EVERY rank drop its own and fall back together - no rank issues
+    the library all-gather while another waits in torch's.  gloo world 4,
+    a stand-in factory."""
+    mp.spawn(_agree_worker, args=(4, _free_port(), fail_rank, str(tmp_path)), nprocs=4,
+             join=True)
+    for r in range(4):
+        has, closed, err = np.load(tmp_path / f"agree{r}.npy")
+        if fail_rank < 0:
+            assert has and not closed and not err
+        else:
+            assert not has and err
+            assert closed == (0 if r == fail_rank else 1)    # the others closed theirs
