@@ -78,7 +78,7 @@ _by_path: dict = {}   # every library loaded, by real path (one CDLL each)
 
 
 def lib_path() -> str:
-    return os.environ.get("EIGEN_VALUE_LIB", DEFAULT_LIB)
+    return os.environ.get("EIGEN_VALUE_LIB") or DEFAULT_LIB
 
 
 def load(path: Optional[str] = None) -> ctypes.CDLL:
@@ -176,6 +176,10 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_set_flat_grid_limit.restype = u32
     L.st_set_defer_caps.argtypes = [i32, i32, u32, u32]
     L.st_set_defer_caps.restype = i32
+    L.st_set_defer_ntload.argtypes = [u32, u32]
+    L.st_set_defer_ntload.restype = i32
+    L.st_defer_ntload_class.argtypes = [u32, u32, i32]
+    L.st_defer_ntload_class.restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32
     L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]

@@ -966,7 +966,7 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool MF = false>
+          int DS = -1, bool MF = false, bool LNT = false>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -1000,6 +1000,8 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
   // compile time (1 / 0; the library's launches), or -1 = pend.store at
   // run time (the sweep tools)
+  // LNT: matrix loads non-temporal on a cached-form launch (the piece size
+  // stays the form's; ST_DEFER_NTLOAD_CACHED)
   // MF: the matrix-free round's sweep (launch k >= 1 of k_mfree's scheme,
   // with FS): `a` is A_0 (read only), `v` is v_{k-2}; each piece's partial
   // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
@@ -1109,14 +1111,14 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     if constexpr (UM) {
 #pragma unroll
       for (int u = 0; u < U; u++)
-        x[u][j] = ld<V, NT>(reinterpret_cast<const V*>(ap + cl[u]));
+        x[u][j] = ld<V, NT || LNT>(reinterpret_cast<const V*>(ap + cl[u]));
       if (r0 + j + 1 < nrows) // uniform
         ap += ncols;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (in[u] && r0 + j < nrows)
-          x[u][j] = ld<V, NT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
+          x[u][j] = ld<V, NT || LNT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
                                                    u * BLK * W));
     }
   }

@@ -775,7 +775,8 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 8192^2 fp64 0.125 vs 0.158; fp32 (every 4th, 4 rows) 0.821 vs 1.350 and
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
-template <typename T, int W, int ORDER, bool NT, int NP, int R, bool STORE>
+template <typename T, int W, int ORDER, bool NT, int NP, int R, bool STORE,
+          bool LNT>
 void
 launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         T* inv_next, T* part, T* v, uint32_t nrows,
@@ -800,7 +801,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   // workgroups per CU (see launch_flat_deferred)
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
                                   kBlock, 0, dev::kGatePlain, NP, U, false,
-                                  STORE ? 1 : 0>),
+                                  STORE ? 1 : 0, false, LNT>),
                      fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
@@ -836,6 +837,45 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   { { 0, 4, 4, 3, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
+
+// Non-temporal matrix loads in the deferred rounds of cached fp64 blocks
+// (below 2 GiB; the launch shapes, piece size and stores stay the cached
+// form's): bit NP (0 ... 4) of a read-only round with NP pending, bit
+// kCapStore of a storing one, by block size class (defer_ntload_class).
+// The solve loop over whole store cycles (tools/defer_profile.py
+// --ntload-ab, 5 interleaved passes, profiles/r03_ntab_*.json), ms per round
+// with the mask shipped vs cached loads throughout:
+//   4096 x 8192 (256 MiB, the 256 MB MALL holds most of it)  0.0474, NT 0x1
+//                                       0.0483 - every NT mask loses
+//   8192^2 (512 MiB)     0x41  0.0954 vs 0.0997 (0x1 0.0955, 0x5f 0.0969)
+//   2880 x 23040 (506 MiB, the P = 8 block)  0x41  0.0982 vs 0.1093
+//   10240^2 (800 MiB)    0x5f  0.1499 vs 0.1586 (0x41 0.1536)
+//   8192 x 16384, 12288^2, 14336^2 (1 - 1.5 GiB)  0x5f  0.1989 / 0.2146 /
+//                        0.3022 vs 0.2071 / 0.2253 / 0.3182
+// The post-store round (NP = 0) reads a matrix the storing round just
+// wrote through the cache; once the block outgrows the MALL those lines
+// only evict each other, and on the larger blocks every read-only round
+// does better streaming past it.
+constexpr int kNtLoadClasses = 3;
+std::atomic<uint32_t> g_defer_ntload[kNtLoadClasses] = { 0u, 0x41u, 0x5fu };
+constexpr uint32_t kNtLoadMask = 0x5fu;
+
+// below 384 MiB, below 640 MiB, above
+inline uint32_t
+defer_ntload_class(size_t bytes)
+{
+  return bytes < ((size_t)384 << 20) ? 0u : bytes < ((size_t)640 << 20) ? 1u : 2u;
+}
+
+template <typename T, bool NT>
+inline uint32_t
+defer_ntload(uint32_t nrows, uint32_t ncols)
+{
+  if (NT || sizeof(T) != 8)
+    return 0u;
+  return g_defer_ntload[defer_ntload_class(block_bytes(nrows, ncols, sizeof(T)))]
+    .load(std::memory_order_relaxed);
+}
 
 template <typename T, bool NT>
 inline uint32_t
@@ -879,20 +919,25 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
+  // cached fp64 blocks: non-temporal loads where g_defer_ntload says so
+  // (the other forms instantiate LNT = false only)
+  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  const uint32_t lnt = defer_ntload<T, NT>(nrows, ncols);
+#define ST_NPL(NPV, RV, STV, LNTV, PTV, LDS)                                   \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, LNTV>(                \
+    a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
+    max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
 #define ST_NP(NPV, RV, PTV, LDS)                                               \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, false>(                    \
-    a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
-    max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
+  (((lnt >> (NPV)) & 1u) ? ST_NPL(NPV, RV, false, kF64C, PTV, LDS)             \
+                         : ST_NPL(NPV, RV, false, false, PTV, LDS))
 #define ST_NPS(NPV, RV, PTV, LDS)                                              \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, true>(                     \
-    a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
-    max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
+  (((lnt >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, kF64C, PTV, LDS)          \
+                             : ST_NPL(NPV, RV, true, false, PTV, LDS))
   // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
   // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
   // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
   // row-major (1 row: 18 % slower at 8192^2 fp32,
   // profiles/r02_flat_map_r1_f32_cached.log)
-  constexpr bool kF64C = !NT && sizeof(T) == 8;
   constexpr int kR0 = NT ? 2 : kF64C ? ST_DEFER_R0_CACHED : 2;
   constexpr uint32_t kTile0 = NT ? 8u : kF64C ? ST_DEFER_PT0_CACHED : 0u;
   constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
@@ -929,6 +974,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
 #undef ST_NP
 #undef ST_NPS
+#undef ST_NPL
 }
 
 template <typename T>
@@ -1585,6 +1631,31 @@ st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
   }
   return (int)st::g_defer_caps[dtype][nontemporal != 0][slot].exchange(
     wg_per_cu, std::memory_order_relaxed);
+}
+
+int
+st_set_defer_ntload(unsigned int size_class, unsigned int mask)
+{
+  st::clear_error();
+  if (size_class >= (unsigned)st::kNtLoadClasses ||
+      (mask & ~st::kNtLoadMask) != 0) {
+    st::set_error("st_set_defer_ntload: size class 0..2, mask of bits 0..4 and 6");
+    return -1;
+  }
+  return (int)st::g_defer_ntload[size_class].exchange(mask,
+                                                      std::memory_order_relaxed);
+}
+
+int
+st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype)
+{
+  st::clear_error();
+  if (dtype != 0 && dtype != 1) {
+    st::set_error("st_defer_ntload_class: dtype 0/1");
+    return -1;
+  }
+  return (int)st::defer_ntload_class(
+    st::block_bytes(nrows, ncols, dtype == 1 ? 8 : 4));
 }
 
 unsigned int

@@ -340,6 +340,19 @@ unsigned int st_set_flat_grid_limit(unsigned int max_x);
 int st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
                       unsigned int wg_per_cu);
 
+/* Non-temporal matrix loads in the deferred flat round's launches on cached
+ * fp64 blocks (below 2 GiB): bit NP (0..4) for a read-only round with NP
+ * pending rounds, bit 6 for a storing round, per block size class
+ * (st_defer_ntload_class: 0 below 384 MiB, 1 below 640 MiB, 2 above).  The
+ * library's defaults are measured (DESIGN.md §Deferred writes); this
+ * overrides one for the process, for tuning tools.  Results do not depend
+ * on it.  Returns the previous mask, or -1 on bad arguments. */
+int st_set_defer_ntload(unsigned int size_class, unsigned int mask);
+
+/* The size class st_set_defer_ntload indexes for an nrows x ncols block
+ * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
+int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);
+
 /* Round k of the flat round with deferred writes (what the solve loops run
  * for blocks where st_round_flat_pays): the matrix in d_mat is the last
  * STORED one, A_j; d_pend_s / d_pend_inv list the npend = k - j pending

@@ -174,3 +174,23 @@ def test_defer_caps_setter():
     old = L.st_set_defer_caps(1, 1, 6, 5)
     assert old >= 0
     assert L.st_set_defer_caps(1, 1, 6, old) == 5
+
+
+def test_defer_ntload_setter():
+    """st_set_defer_ntload (non-temporal loads of the cached fp64 deferred
+    rounds) and its size classes: bad arguments are refused, the shipped
+    masks are the measured ones, a mask set is returned by the
+    next call."""
+    L = _lib.load()
+    assert L.st_set_defer_ntload(3, 0) < 0 and "st_set_defer_ntload" in _lib.last_error()
+    assert L.st_set_defer_ntload(0, 0x20) < 0 and L.st_set_defer_ntload(0, 0x80) < 0
+    assert L.st_defer_ntload_class(8192, 8192, 2) < 0
+    assert [L.st_defer_ntload_class(r, c, 1) for r, c in
+            ((4096, 8192), (8192, 8192), (2880, 23040), (10240, 10240), (12288, 12288))] == [0, 1, 1, 2, 2]
+    assert L.st_defer_ntload_class(8192, 8192, 0) == 0          # fp32: 256 MiB
+    shipped = []
+    for cls in range(3):
+        old = L.st_set_defer_ntload(cls, 0x41)
+        shipped.append(old)
+        assert L.st_set_defer_ntload(cls, old) == 0x41
+    assert shipped == [0, 0x41, 0x5f]

@@ -48,11 +48,21 @@ def set_caps(spec, dtype, n, elem, nrows=None):
         _lib.check(L.st_set_defer_caps(1 if dtype == "f64" else 0, nt, slot, c), "caps")
 
 
+def set_ntload(mask, n, elem, nrows=None):
+    """--ntload-ab: the non-temporal-load mask of the deferred launches on
+    cached fp64 blocks (st_set_defer_ntload; bit NP 0..4 = read-only round
+    with NP pending, bit 6 = storing round) for this block's size class."""
+    from eigen_value_amd import _lib
+    L = _lib.load()
+    cls = L.st_defer_ntload_class(nrows or n, n, 1 if elem == 8 else 0)
+    _lib.check(L.st_set_defer_ntload(cls, int(mask, 0)), "ntload")
+
+
 def run_caps_ab(args):
-    """--caps-ab 'spec;spec;...': the same store cycles under each caps spec
-    (st_set_defer_caps), interleaved over --passes repeats so that clock
-    drift hits every spec alike; prints and returns the median ms per round
-    of each spec."""
+    """--caps-ab 'spec;spec;...' (st_set_defer_caps) or --ntload-ab
+    'mask;mask;...' (st_set_defer_ntload): the same store cycles under each
+    spec, interleaved over --passes repeats so that clock drift hits every
+    spec alike; prints and returns the median ms per round of each spec."""
     import torch
     import bench
     from eigen_value_amd import sharded
@@ -62,13 +72,22 @@ def run_caps_ab(args):
     sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb)
     assert sh.deferred_writes
     sh.load(args.kind, seed=0)
-    specs = args.caps_ab.split(";")
+    if args.ntload_ab:
+        what, specs = "ntload", args.ntload_ab.split(";")
+
+        def apply(sp):
+            set_ntload(sp, args.n, elem, sh.part.nrows)
+    else:
+        what, specs = "caps", args.caps_ab.split(";")
+
+        def apply(sp):
+            set_caps(sp, args.dtype, args.n, elem, sh.part.nrows)
     res = {sp: [] for sp in specs}
-    set_caps(specs[0], args.dtype, args.n, elem, sh.part.nrows)
+    apply(specs[0])
     bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)          # warm-up
     for _ in range(args.passes):
         for sp in specs:
-            set_caps(sp, args.dtype, args.n, elem, sh.part.nrows)
+            apply(sp)
             res[sp].append(bench.timed_deferred(sh, args.cycles, 0, torch, None, 1)[1])
     out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
                f" rank 0 of {args.rank_block}" if args.rank_block else ""),
@@ -76,7 +95,7 @@ def run_caps_ab(args):
     for sp in specs:
         v = sorted(res[sp])
         out["ms_per_round"][sp] = {"median": v[len(v) // 2], "min": v[0], "max": v[-1]}
-        print(f"{out['workload']} caps {sp:24s} median {v[len(v) // 2]:.5f} ms/round "
+        print(f"{out['workload']} {what} {sp:24s} median {v[len(v) // 2]:.5f} ms/round "
               f"(min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
     sh.close()
     return out
@@ -89,11 +108,14 @@ def run(args):
     if args.caps:
         set_caps(args.caps, args.dtype, args.n, 8 if args.dtype == "f64" else 4)
     dt = torch.float64 if args.dtype == "f64" else torch.float32
-    sh = sharded.ShardedSimilarityTransform(args.n, dt)
+    rb = (args.rank_block, 0) if args.rank_block else None
+    sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb)
     assert sh.deferred_writes, "block below the flat-round size: no deferred writes"
     sh.load(args.kind, seed=0)
     el, ev_ms, m = bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)
-    out = {"workload": f"{args.kind}{args.n}_{args.dtype}", "m": m, "cycles": args.cycles,
+    out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
+               f" rank 0 of {args.rank_block}" if args.rank_block else ""),
+           "m": m, "cycles": args.cycles,
            "event_ms_per_round": ev_ms, "host_ms_per_round": el / (args.cycles * m) * 1e3,
            "caps": args.caps}
     if args.passes > 1:   # more passes over the same cycles (the first warmed up above)
@@ -219,15 +241,17 @@ if __name__ == "__main__":
                                   "slots 0..6 comma-separated (st_set_defer_caps)")
     p.add_argument("--passes", type=int, default=1, help="run mode: timed passes (median)")
     p.add_argument("--caps-ab", help="A/B of caps specs separated by ';' (interleaved passes)")
+    p.add_argument("--ntload-ab", help="A/B of non-temporal-load masks (cached fp64 blocks) "
+                                       "separated by ';', e.g. '0;0x1;0x41'")
     p.add_argument("--ab-json", help="with --caps-ab: write the medians here")
     p.add_argument("--rank-block", type=int, default=0,
-                   help="with --caps-ab: rank 0's block of a P-way row partition (no exchange)")
+                   help="rank 0's block of a P-way row partition (no exchange)")
     p.add_argument("--write")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.caps_ab:
+    if a.caps_ab or a.ntload_ab:
         r = run_caps_ab(a)
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)

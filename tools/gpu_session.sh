@@ -97,6 +97,40 @@ for s in $STEPS; do
       step capsab3_f64_6144 300 python3 tools/defer_profile.py --kind random --n 6144 --dtype f64 --cycles 60 --passes 7 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_random6144_f64.json"
       step capsab3_f64_p8w 300 python3 tools/defer_profile.py --kind hilbert --n 23040 --rank-block 8 --dtype f64 --cycles 40 --passes 7 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_hilbert23040_p8_f64.json"
       step capsab3_f32_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f32 --cycles 60 --passes 7 --caps-ab "$F32C_SPECS" --ab-json "$OUT/${RTAG}_capsab3_hilbert8192_f32.json" ;;
+    libab) # whole store cycles under probe builds of the library (tools/defer_shape_probe.sh
+           # variants in eigen_value_amd/lib/variants/NAME), interleaved with the shipped one
+      for rep in 1 2 3; do
+        for V in base $LIBAB_VARIANTS; do
+          if [ "$V" = base ]; then LIBV=""; else LIBV="eigen_value_amd/lib/variants/$V/libsimilarity_transform.so"; fi
+          EIGEN_VALUE_LIB=$LIBV step "libab_${V}_$rep" 200 python3 tools/defer_profile.py --kind ${LIBAB_KIND:-hilbert} --n ${LIBAB_N:-8192} --dtype ${LIBAB_DT:-f64} --cycles ${LIBAB_CYCLES:-40} --passes 3 ${LIBAB_EXTRA:-} --events "$OUT/libab_${V}_$rep.json"
+        done
+      done
+      python3 - "$OUT" <<'PY' | tee -a "$OUT/session.log"
+import glob, json, os, sys, collections
+r = collections.defaultdict(list)
+for f in sorted(glob.glob(os.path.join(sys.argv[1], "libab_*.json"))):
+    v = os.path.basename(f)[6:].rsplit("_", 1)[0]
+    r[v].append(json.load(open(f))["event_ms_per_round"])
+for v, xs in r.items():
+    xs = sorted(xs)
+    print(f"libab {v:16s} ms/round {xs}  median {xs[len(xs) // 2]:.5f}")
+PY
+      ;;
+    ntab) # non-temporal-load masks of the cached fp64 deferred rounds (st_set_defer_ntload),
+          # interleaved passes over whole store cycles
+      M_SPECS=${NTAB_SPECS:-"0;0x1;0x41;0x5f;0x3;0x43;0x1f"}
+      for W in "hilbert 8192 0" "hilbert 8192 2" "hilbert 23040 8" "random 10240 0" "random 12288 0" "random 14336 0" "random 16384 2"; do
+        set -- $W; K=$1; N=$2; P=$3
+        step "ntab_${K}${N}_p$P" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype f64 --cycles 40 --passes 5 --ntload-ab "$M_SPECS" --ab-json "$OUT/${RTAG}_ntab_${K}${N}_p${P}_f64.json"
+        grep ntload "$OUT/ntab_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
+      done ;;
+    capsab4) # cached fp64 caps again, now that rounds load non-temporally (g_defer_ntload)
+      C_SPECS="0,4,4,3,3,0,3;0,0,0,0,0,0,0;0,5,4,4,4,0,3;4,4,4,3,3,0,3;0,4,4,3,3,0,4;0,4,4,3,3,0,2;0,5,5,4,4,0,3"
+      for W in "hilbert 8192 0" "hilbert 23040 8" "random 12288 0"; do
+        set -- $W; K=$1; N=$2; P=$3
+        step "capsab4_${K}${N}_p$P" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype f64 --cycles 40 --passes 5 --caps-ab "$C_SPECS" --ab-json "$OUT/${RTAG}_capsab4_${K}${N}_p${P}_f64.json"
+        grep caps "$OUT/capsab4_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
+      done ;;
     sq) # SQ instruction / wait counters of the deferred launches (two PMC passes)
       C1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY"
       C2="SQ_WAVES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_BUSY_CYCLES"
