@@ -966,7 +966,7 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool MF = false, bool LNT = false>
+          int DS = -1, bool MF = false, bool LNT = false, int FLIP = 0>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -1002,6 +1002,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // run time (the sweep tools)
   // LNT: matrix loads non-temporal on a cached-form launch (the piece size
   // stays the form's; ST_DEFER_NTLOAD_CACHED)
+  // FLIP: the every-round launch's cache policy (st_set_every_cache): bit 0
+  // turns the matrix loads' policy over (cached <-> non-temporal), bit 1
+  // the stores'; the shapes stay the form's
   // MF: the matrix-free round's sweep (launch k >= 1 of k_mfree's scheme,
   // with FS): `a` is A_0 (read only), `v` is v_{k-2}; each piece's partial
   // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
@@ -1097,7 +1100,8 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   const bool do_store = NP < 0 || (DS >= 0 ? DS == 1 : pend.store != 0); // uniform
   // the deferred rounds' stores (probe switch ST_DEFER_STORE_NT: non-temporal
   // on cached blocks too)
-  constexpr bool NTS = NT || (NP >= 0 && ST_DEFER_STORE_NT);
+  constexpr bool NTS = (NT || (NP >= 0 && ST_DEFER_STORE_NT)) != ((FLIP & 2) != 0);
+  constexpr bool NTL = (NT || LNT) != ((FLIP & 1) != 0);
   uint32_t cl[U]; // the column each lane loads
 #pragma unroll
   for (int u = 0; u < U; u++)
@@ -1111,14 +1115,14 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     if constexpr (UM) {
 #pragma unroll
       for (int u = 0; u < U; u++)
-        x[u][j] = ld<V, NT || LNT>(reinterpret_cast<const V*>(ap + cl[u]));
+        x[u][j] = ld<V, NTL>(reinterpret_cast<const V*>(ap + cl[u]));
       if (r0 + j + 1 < nrows) // uniform
         ap += ncols;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (in[u] && r0 + j < nrows)
-          x[u][j] = ld<V, NT || LNT>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
+          x[u][j] = ld<V, NTL>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
                                                    u * BLK * W));
     }
   }

@@ -254,6 +254,45 @@ flat_every_tile(uint32_t nrows, uint32_t ncols)
   return block_bytes(nrows, ncols, sizeof(T)) >= ((size_t)384 << 20) ? 8u : 4u;
 }
 
+// Cache policy of the every-round flat launch, by block size class
+// (every_cache_class: below 384 MiB, below 640 MiB, below 2 GiB - the cached
+// form - and from 2 GiB - the non-temporal form): bit 0 turns the matrix
+// loads' policy over (cached <-> non-temporal), bit 1 the stores'; the
+// shapes, piece size and piece order stay the form's.  Set per class for
+// tools by st_set_every_cache; results do not depend on it.  The bench's
+// timed step (tools/defer_profile.py --every-ab, 5 - 10 interleaved passes
+// of 100 rounds, two boxes, profiles/r03_everyab_*.json), ms per round:
+//   policy         0 (form's)   1 (nt loads)   2 (nt stores)  3 (both)
+//   8192^2 fp64    0.1555/0.1558   0.1625        0.1533/0.1528   0.1747
+//   2880 x 23040   0.1470/0.1469   0.1678        0.1467/0.1462   0.1776
+//   5824 x 11648   0.1560/0.1564   0.1790        0.1557/0.1554   0.1840
+//   4096 x 16384   0.1469/0.1472   0.1573        0.1462/0.1462   0.1734
+//   6144^2 fp64    0.0878/0.0882   0.1011        0.0876/0.0882   0.1020
+//   8192^2 fp32    0.0764/0.0764   0.0833        0.0759/0.0760   0.0878
+//   12288^2 fp32   0.1760/0.1760   0.1920        0.1755/0.1752   0.1978
+//   10240^2 fp64   0.2594/0.2595   0.2760        0.2605/0.2603   0.2755
+//   12288^2 fp64   0.3845/0.3848   0.4026        0.3858/0.3853   0.3947
+//   16384^2 fp32   0.3262/0.3257   0.3474        0.3260/0.3253   0.3370
+//   (non-temporal form: 1 = cached loads, 2 = cached stores, 3 = both)
+//   32768^2 fp64   2.643           3.180          2.944          3.226
+//   8192 x 65536   1.349           1.632          1.464          1.635
+//   32768^2 fp32   1.308           1.426          1.466          1.425
+// Streaming the stores past the caches pays while the block is at most
+// about twice the 256 MB memory-side cache (8192^2 fp64 -1.9 %), not above;
+// loads stay cached there (the next round's first pieces are read from the
+// cache), and the non-temporal form keeps both non-temporal.
+constexpr int kEveryCacheClasses = 4;
+std::atomic<uint32_t> g_every_cache[kEveryCacheClasses] = { 2u, 2u, 0u, 0u };
+
+inline uint32_t
+every_cache_class(size_t bytes)
+{
+  return bytes < ((size_t)384 << 20)   ? 0u
+         : bytes < ((size_t)640 << 20) ? 1u
+         : bytes < ((size_t)2 << 30)   ? 2u
+                                       : 3u;
+}
+
 // k_parts of an unsplit flat round: rows of <= 16 / 32 partials take 4 / 2
 // rows per wave (k_parts_seg, bitwise k_parts' sums), longer ones a wave
 // each (k_parts)
@@ -698,13 +737,26 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
   pe.pt = flat_every_tile<T, NT>(nrows, ncols);
   if constexpr (kFlatFusedStats) {
     // two launches: m_k / stop_k folded into k_flat's first row group, the
-    // v update into k_parts
-    hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,
-                   dev::kGatePlain, -1, U>),
-      fg.grid,
-      dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr, row0, k,
-      st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
+    // v update into k_parts; the cache policy of the matrix loads / stores
+    // per g_every_cache (vector path only)
+    const uint32_t pol =
+      W == 1 ? 0u
+             : g_every_cache[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))]
+                 .load(std::memory_order_relaxed);
+#define ST_EVERY(FL)                                                           \
+  hipLaunchKernelGGL(                                                          \
+    (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,         \
+                 dev::kGatePlain, -1, U, false, -1, false, false, FL>),        \
+    fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,    \
+    row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
+    constexpr int kV = W > 1 ? 1 : 0;
+    switch (pol) {
+      case 1u: ST_EVERY(kV); break;
+      case 2u: ST_EVERY(2 * kV); break;
+      case 3u: ST_EVERY(3 * kV); break;
+      default: ST_EVERY(0); break;
+    }
+#undef ST_EVERY
     launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr, stream);
   } else {
     const uint32_t sgrid =
@@ -776,7 +828,7 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
 template <typename T, int W, int ORDER, bool NT, int NP, int R, bool STORE,
-          bool LNT>
+          bool LNT, int FL = 0>
 void
 launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         T* inv_next, T* part, T* v, uint32_t nrows,
@@ -801,7 +853,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   // workgroups per CU (see launch_flat_deferred)
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
                                   kBlock, 0, dev::kGatePlain, NP, U, false,
-                                  STORE ? 1 : 0, false, LNT>),
+                                  STORE ? 1 : 0, false, LNT, FL>),
                      fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
@@ -858,7 +910,9 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
 // does better streaming past it.
 constexpr int kNtLoadClasses = 3;
 std::atomic<uint32_t> g_defer_ntload[kNtLoadClasses] = { 0u, 0x41u, 0x5fu };
-constexpr uint32_t kNtLoadMask = 0x5fu;
+// bit 7: the storing round's stores non-temporal too
+constexpr uint32_t kNtStoreBit = 7u;
+constexpr uint32_t kNtLoadMask = 0xdfu;
 
 // below 384 MiB, below 640 MiB, above
 inline uint32_t
@@ -930,9 +984,17 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 #define ST_NP(NPV, RV, PTV, LDS)                                               \
   (((lnt >> (NPV)) & 1u) ? ST_NPL(NPV, RV, false, kF64C, PTV, LDS)             \
                          : ST_NPL(NPV, RV, false, false, PTV, LDS))
+#define ST_NPLF(NPV, RV, LNTV, PTV, LDS)                                       \
+  (((lnt >> kNtStoreBit) & 1u)                                                 \
+     ? launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, true, LNTV,           \
+                               kF64C ? 2 : 0>(                                 \
+         a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0,     \
+         eps, k, max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS,    \
+         stream)                                                               \
+     : ST_NPL(NPV, RV, true, LNTV, PTV, LDS))
 #define ST_NPS(NPV, RV, PTV, LDS)                                              \
-  (((lnt >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, kF64C, PTV, LDS)          \
-                             : ST_NPL(NPV, RV, true, false, PTV, LDS))
+  (((lnt >> kCapStore) & 1u) ? ST_NPLF(NPV, RV, kF64C, PTV, LDS)               \
+                             : ST_NPLF(NPV, RV, false, PTV, LDS))
   // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
   // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
   // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
@@ -974,6 +1036,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
 #undef ST_NP
 #undef ST_NPS
+#undef ST_NPLF
 #undef ST_NPL
 }
 
@@ -1639,7 +1702,7 @@ st_set_defer_ntload(unsigned int size_class, unsigned int mask)
   st::clear_error();
   if (size_class >= (unsigned)st::kNtLoadClasses ||
       (mask & ~st::kNtLoadMask) != 0) {
-    st::set_error("st_set_defer_ntload: size class 0..2, mask of bits 0..4 and 6");
+    st::set_error("st_set_defer_ntload: size class 0..2, mask of bits 0..4, 6 and 7");
     return -1;
   }
   return (int)st::g_defer_ntload[size_class].exchange(mask,
@@ -1655,6 +1718,30 @@ st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype)
     return -1;
   }
   return (int)st::defer_ntload_class(
+    st::block_bytes(nrows, ncols, dtype == 1 ? 8 : 4));
+}
+
+int
+st_set_every_cache(unsigned int size_class, unsigned int policy)
+{
+  st::clear_error();
+  if (size_class >= (unsigned)st::kEveryCacheClasses || policy > 3u) {
+    st::set_error("st_set_every_cache: size class 0..3, policy 0..3");
+    return -1;
+  }
+  return (int)st::g_every_cache[size_class].exchange(policy,
+                                                     std::memory_order_relaxed);
+}
+
+int
+st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype)
+{
+  st::clear_error();
+  if (dtype != 0 && dtype != 1) {
+    st::set_error("st_every_cache_class: dtype 0/1");
+    return -1;
+  }
+  return (int)st::every_cache_class(
     st::block_bytes(nrows, ncols, dtype == 1 ? 8 : 4));
 }
 

@@ -342,7 +342,8 @@ int st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
 
 /* Non-temporal matrix loads in the deferred flat round's launches on cached
  * fp64 blocks (below 2 GiB): bit NP (0..4) for a read-only round with NP
- * pending rounds, bit 6 for a storing round, per block size class
+ * pending rounds, bit 6 for a storing round (bit 7: its stores non-temporal
+ * as well), per block size class
  * (st_defer_ntload_class: 0 below 384 MiB, 1 below 640 MiB, 2 above).  The
  * library's defaults are measured (DESIGN.md §Deferred writes); this
  * overrides one for the process, for tuning tools.  Results do not depend
@@ -352,6 +353,20 @@ int st_set_defer_ntload(unsigned int size_class, unsigned int mask);
 /* The size class st_set_defer_ntload indexes for an nrows x ncols block
  * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
 int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);
+
+/* Cache policy of the every-round flat launch (the vector path): bit 0 turns
+ * the matrix loads' policy over (cached <-> non-temporal), bit 1 the
+ * stores', 0 = the form's own, per block size class (st_every_cache_class:
+ * 0 below 384 MiB, 1 below 640 MiB, 2 below 2 GiB - the cached form - and
+ * 3 from 2 GiB - the non-temporal form).  The library's defaults are
+ * measured; this overrides one for the process, for
+ * tuning tools.  Results do not depend on it.  Returns the previous policy,
+ * or -1 on bad arguments. */
+int st_set_every_cache(unsigned int size_class, unsigned int policy);
+
+/* The size class st_set_every_cache indexes for an nrows x ncols block
+ * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
+int st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype);
 
 /* Round k of the flat round with deferred writes (what the solve loops run
  * for blocks where st_round_flat_pays): the matrix in d_mat is the last

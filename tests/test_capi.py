@@ -183,7 +183,7 @@ def test_defer_ntload_setter():
     next call."""
     L = _lib.load()
     assert L.st_set_defer_ntload(3, 0) < 0 and "st_set_defer_ntload" in _lib.last_error()
-    assert L.st_set_defer_ntload(0, 0x20) < 0 and L.st_set_defer_ntload(0, 0x80) < 0
+    assert L.st_set_defer_ntload(0, 0x20) < 0 and L.st_set_defer_ntload(0, 0x100) < 0
     assert L.st_defer_ntload_class(8192, 8192, 2) < 0
     assert [L.st_defer_ntload_class(r, c, 1) for r, c in
             ((4096, 8192), (8192, 8192), (2880, 23040), (10240, 10240), (12288, 12288))] == [0, 1, 1, 2, 2]
@@ -194,3 +194,24 @@ def test_defer_ntload_setter():
         shipped.append(old)
         assert L.st_set_defer_ntload(cls, old) == 0x41
     assert shipped == [0, 0x41, 0x5f]
+
+
+def test_every_cache_setter():
+    """st_set_every_cache (the every-round flat launch's cache policy on
+    cached blocks) and its size classes: bad arguments are refused, the
+    shipped policies are the measured ones, a policy set is
+    returned by the next call."""
+    L = _lib.load()
+    assert L.st_set_every_cache(4, 0) < 0 and "st_set_every_cache" in _lib.last_error()
+    assert L.st_set_every_cache(0, 4) < 0
+    assert L.st_every_cache_class(8192, 8192, 2) < 0
+    assert [L.st_every_cache_class(r, c, 1) for r, c in
+            ((4096, 8192), (8192, 8192), (2880, 23040), (10240, 10240), (32768, 32768))] \
+        == [0, 1, 1, 2, 3]
+    assert L.st_set_every_cache(4, 0) < 0
+    shipped = []
+    for cls in range(4):
+        old = L.st_set_every_cache(cls, 3)
+        shipped.append(old)
+        assert L.st_set_every_cache(cls, old) == 3
+    assert shipped == [2, 2, 0, 0]

@@ -1181,9 +1181,10 @@ def test_deferred_caps_do_not_change_results(solver, dt, n):
 def test_deferred_ntload_does_not_change_results(solver, n):
     """Non-temporal matrix loads in the cached fp64 deferred rounds
     (st_set_defer_ntload, per block size class) change the cache policy
-    only: a solve under the shipped mask, with cached loads throughout and
-    with every round's loads non-temporal is bit-identical (λ, v,
-    iterations, final matrix)."""
+    only: a solve under the shipped mask, with cached loads throughout, with
+    every round's loads non-temporal and with the storing round's stores
+    non-temporal too (bit 7) is bit-identical (λ, v, iterations, final
+    matrix)."""
     L = _lib.load()
     cls = L.st_defer_ntload_class(n, n, 1)
     assert cls == {4352: 0, 8192: 1, 10240: 2}[n]
@@ -1191,7 +1192,7 @@ def test_deferred_ntload_does_not_change_results(solver, n):
     saved = L.st_set_defer_ntload(cls, 0)
     try:
         out = []
-        for mask in (saved, 0, 0x5f):
+        for mask in (saved, 0, 0x5f, 0xdf):
             assert L.st_set_defer_ntload(cls, mask) >= 0
             a = base.clone()
             r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
@@ -1201,6 +1202,31 @@ def test_deferred_ntload_does_not_change_results(solver, n):
             assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
     finally:
         L.st_set_defer_ntload(cls, saved)
+
+
+@pytest.mark.parametrize("n", [4352, 8192, 10240])
+def test_every_cache_does_not_change_results(solver, n):
+    """The every-round flat launch's cache policy (st_set_every_cache: the
+    loads', the stores' or both policies turned over, per block size class)
+    changes where lines are kept only: a solve that stores every round is
+    bit-identical under every policy (λ, v, iterations, final matrix)."""
+    L = _lib.load()
+    cls = L.st_every_cache_class(n, n, 1)
+    assert cls == {4352: 0, 8192: 1, 10240: 2}[n]
+    base = dev.generate("random", n, torch.float64, seed=11, device=DEV)
+    saved = L.st_set_every_cache(cls, 0)
+    try:
+        out = []
+        for pol in (saved, 0, 1, 2, 3):
+            assert L.st_set_every_cache(cls, pol) >= 0
+            a = base.clone()
+            r = solver.solve(a, inplace=True, eps=0.0, max_itr=7, write_every_round=True)
+            out.append((r[0], r[2], r[1].cpu(), a))
+        for o in out[1:]:
+            assert o[0] == out[0][0] and o[1] == out[0][1]
+            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
+    finally:
+        L.st_set_every_cache(cls, saved)
 
 
 @pytest.mark.parametrize("limit", [8, 1000, 4096])

@@ -58,6 +58,51 @@ def set_ntload(mask, n, elem, nrows=None):
     _lib.check(L.st_set_defer_ntload(cls, int(mask, 0)), "ntload")
 
 
+def set_every(policy, n, elem, nrows=None):
+    """--every-ab: the cache policy of the every-round flat launch
+    (st_set_every_cache: 0 the form's own, 1 / 2 / 3 turn the loads' /
+    stores' / both policies over, cached <-> non-temporal) for this block's
+    size class."""
+    from eigen_value_amd import _lib
+    L = _lib.load()
+    cls = L.st_every_cache_class(nrows or n, n, 1 if elem == 8 else 0)
+    _lib.check(L.st_set_every_cache(cls, int(policy, 0)), "every_cache")
+
+
+def run_every_ab(args):
+    """--every-ab 'p;p;...': the every-round flat round (bench.py's timed
+    step) under each cache policy, --steps rounds per pass, interleaved over
+    --passes repeats; prints and returns the median ms per round of each."""
+    import torch
+    import bench
+    from eigen_value_amd import sharded
+    elem = 8 if args.dtype == "f64" else 4
+    dt = torch.float64 if args.dtype == "f64" else torch.float32
+    rb = (args.rank_block, 0) if args.rank_block else None
+    sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb)
+    sh.load(args.kind, seed=0)
+    specs = args.every_ab.split(";")
+    res = {sp: [] for sp in specs}
+    set_every(specs[0], args.n, elem, sh.part.nrows)
+    bench.timed_rounds(sh, args.steps, 10, torch, None, 1)             # warm-up
+    for _ in range(args.passes):
+        for sp in specs:
+            set_every(sp, args.n, elem, sh.part.nrows)
+            res[sp].append(bench.timed_rounds(sh, args.steps, 4, torch, None, 1)[1])
+    out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
+               f" rank 0 of {args.rank_block}" if args.rank_block else ""),
+           "form": "every-round flat round (k_flat + k_parts)",
+           "steps": args.steps, "passes": args.passes, "ms_per_round": {}}
+    for sp in specs:
+        v = sorted(res[sp])
+        out["ms_per_round"][sp] = {"median": v[len(v) // 2], "min": v[0], "max": v[-1]}
+        print(f"{out['workload']} every-cache {sp:6s} median {v[len(v) // 2]:.5f} ms/round "
+              f"(min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
+    set_every("0", args.n, elem, sh.part.nrows)
+    sh.close()
+    return out
+
+
 def run_caps_ab(args):
     """--caps-ab 'spec;spec;...' (st_set_defer_caps) or --ntload-ab
     'mask;mask;...' (st_set_defer_ntload): the same store cycles under each
@@ -243,7 +288,10 @@ if __name__ == "__main__":
     p.add_argument("--caps-ab", help="A/B of caps specs separated by ';' (interleaved passes)")
     p.add_argument("--ntload-ab", help="A/B of non-temporal-load masks (cached fp64 blocks) "
                                        "separated by ';', e.g. '0;0x1;0x41'")
-    p.add_argument("--ab-json", help="with --caps-ab: write the medians here")
+    p.add_argument("--every-ab", help="A/B of every-round cache policies (st_set_every_cache: "
+                   "0 the form's, 1 / 2 / 3 loads / stores / both turned over) separated by ';'")
+    p.add_argument("--steps", type=int, default=100, help="with --every-ab: rounds per pass")
+    p.add_argument("--ab-json", help="with --caps-ab / --every-ab: write the medians here")
     p.add_argument("--rank-block", type=int, default=0,
                    help="rank 0's block of a P-way row partition (no exchange)")
     p.add_argument("--write")
@@ -251,8 +299,8 @@ if __name__ == "__main__":
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.caps_ab or a.ntload_ab:
-        r = run_caps_ab(a)
+    if a.caps_ab or a.ntload_ab or a.every_ab:
+        r = run_every_ab(a) if a.every_ab else run_caps_ab(a)
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)
     elif a.trace or a.fetch:

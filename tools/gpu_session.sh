@@ -124,6 +124,23 @@ PY
         step "ntab_${K}${N}_p$P" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype f64 --cycles 40 --passes 5 --ntload-ab "$M_SPECS" --ab-json "$OUT/${RTAG}_ntab_${K}${N}_p${P}_f64.json"
         grep ntload "$OUT/ntab_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
       done ;;
+    everyab) # cache policy of the every-round flat launch (st_set_every_cache: 1 / 2 / 3 turn
+             # the loads' / stores' / both policies over, cached <-> non-temporal),
+             # interleaved passes of the bench's timed step
+      E_SPECS=${EVERYAB_SPECS:-"0;1;2;3"}
+      for W in ${EVERYAB_CASES:-hilbert,8192,0,f64 hilbert,23040,8,f64 hilbert,11648,2,f64 hilbert,16384,4,f64 random,6144,0,f64 random,10240,0,f64 random,12288,0,f64 hilbert,8192,0,f32 random,12288,0,f32 random,16384,0,f32 random,32768,0,f64 random,65536,8,f64 random,32768,0,f32}; do
+        set -- ${W//,/ }; K=$1; N=$2; P=$3; D=$4
+        step "everyab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 100 --passes 5 --every-ab "$E_SPECS" --ab-json "$OUT/${RTAG}_everyab_${K}${N}_p${P}_$D.json"
+        grep every-cache "$OUT/everyab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
+      done ;;
+    ntab2) # bit 7 of the cached fp64 deferred mask: the storing round's stores non-temporal
+      for W in "hilbert 8192 0 0x41;0xc1;0x1;0x81" "hilbert 23040 8 0x41;0xc1" "hilbert 11648 2 0x41;0xc1" "random 10240 0 0x5f;0xdf" "random 12288 0 0x5f;0xdf" "random 6144 0 0;0x80;0x41;0xc1"; do
+        set -- $W; K=$1; N=$2; P=$3; M=$4
+        step "ntab2_${K}${N}_p$P" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype f64 --cycles 40 --passes 7 --ntload-ab "$M" --ab-json "$OUT/${RTAG}_ntab2_${K}${N}_p${P}_f64.json"
+        grep ntload "$OUT/ntab2_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
+      done ;;
+    cachetests) # the bitwise tests of the cache-policy switches
+      step pytest_cache 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "every_cache or ntload" ;;
     capsab4) # cached fp64 caps again, now that rounds load non-temporally (g_defer_ntload)
       C_SPECS="0,4,4,3,3,0,3;0,0,0,0,0,0,0;0,5,4,4,4,0,3;4,4,4,3,3,0,3;0,4,4,3,3,0,4;0,4,4,3,3,0,2;0,5,5,4,4,0,3"
       for W in "hilbert 8192 0" "hilbert 23040 8" "random 12288 0"; do
