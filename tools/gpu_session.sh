@@ -190,8 +190,8 @@ PY
     profile)
       # one workload per profiled command, so every rocprofv3 summary row
       # belongs to a single launch shape: configs[1] and the north-star size
-      for W in "hilbert 8192" "random 32768"; do
-        set -- $W; K=$1; N=$2; D="$OUT/${K}${N}"
+      for W in ${PROFILE_CASES:-hilbert,8192 random,32768}; do
+        set -- ${W//,/ }; K=$1; N=$2; D="$OUT/${K}${N}"
         step "prof_${K}${N}" 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$D/prof" -o run -- python3 bench.py --kind $K --n $N --no-cpu --no-north-star --no-headline
         step "pmc_fetch_${K}${N}" 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$D/pmc_fetch" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
         step "pmc_write_${K}${N}" 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$D/pmc_write" -o run -- python3 bench.py --kind $K --n $N --steps 20 --warmup 2 --no-cpu --no-north-star --no-headline
