@@ -243,10 +243,23 @@ template <typename T, bool NT>
 constexpr int kFlatEveryRows =
   (sizeof(T) == 8 && !NT && ST_EVERY_CACHED_R1) ? 1 : kFlatRows;
 
+// tools: the every-round launch's piece tile per size class
+// (every_cache_class; 0 = the table below, 1 = row-major, t = tiles of t row
+// groups), st_set_every_tile
+constexpr int kEveryTileClasses = 4;
+std::atomic<uint32_t> g_every_tile[kEveryTileClasses] = { 0u, 0u, 0u, 0u };
+
+inline uint32_t every_cache_class(size_t bytes);
+
 template <typename T, bool NT>
 inline uint32_t
 flat_every_tile(uint32_t nrows, uint32_t ncols)
 {
+  const uint32_t ov =
+    g_every_tile[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))].load(
+      std::memory_order_relaxed);
+  if (ov != 0)
+    return ov == 1 ? 0u : ov;
   if (NT)
     return 4u;
   if (sizeof(T) == 4 || !ST_EVERY_CACHED_R1)
@@ -1731,6 +1744,17 @@ st_set_every_cache(unsigned int size_class, unsigned int policy)
   }
   return (int)st::g_every_cache[size_class].exchange(policy,
                                                      std::memory_order_relaxed);
+}
+
+int
+st_set_every_tile(unsigned int size_class, unsigned int tile)
+{
+  st::clear_error();
+  if (size_class >= (unsigned)st::kEveryTileClasses || tile > 4096u) {
+    st::set_error("st_set_every_tile: size class 0..3, tile 0..4096");
+    return -1;
+  }
+  return (int)st::g_every_tile[size_class].exchange(tile, std::memory_order_relaxed);
 }
 
 int

@@ -364,6 +364,12 @@ int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);
  * or -1 on bad arguments. */
 int st_set_every_cache(unsigned int size_class, unsigned int policy);
 
+/* Piece order of the every-round flat launch per size class (the classes of
+ * st_set_every_cache): 0 = the library's measured table, 1 = row-major,
+ * t > 1 = tiles of t row groups per piece.  For tuning tools; results do not
+ * depend on it.  Returns the previous value, or -1 on bad arguments. */
+int st_set_every_tile(unsigned int size_class, unsigned int tile);
+
 /* The size class st_set_every_cache indexes for an nrows x ncols block
  * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
 int st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype);

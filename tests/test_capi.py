@@ -215,3 +215,5 @@ def test_every_cache_setter():
         shipped.append(old)
         assert L.st_set_every_cache(cls, old) == 3
     assert shipped == [2, 2, 0, 0]
+    assert L.st_set_every_tile(4, 0) < 0 and L.st_set_every_tile(0, 4097) < 0
+    assert L.st_set_every_tile(1, 16) == 0 and L.st_set_every_tile(1, 0) == 16

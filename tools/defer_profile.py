@@ -62,11 +62,14 @@ def set_every(policy, n, elem, nrows=None):
     """--every-ab: the cache policy of the every-round flat launch
     (st_set_every_cache: 0 the form's own, 1 / 2 / 3 turn the loads' /
     stores' / both policies over, cached <-> non-temporal) for this block's
-    size class."""
+    size class; "P:T" also sets the piece tile (st_set_every_tile: 1 =
+    row-major, t = tiles of t row groups, 0 = the library's table)."""
     from eigen_value_amd import _lib
     L = _lib.load()
     cls = L.st_every_cache_class(nrows or n, n, 1 if elem == 8 else 0)
-    _lib.check(L.st_set_every_cache(cls, int(policy, 0)), "every_cache")
+    pol, _, tile = policy.partition(":")      # "P" or "P:T" (T: st_set_every_tile)
+    _lib.check(L.st_set_every_cache(cls, int(pol, 0)), "every_cache")
+    _lib.check(L.st_set_every_tile(cls, int(tile or "0", 0)), "every_tile")
 
 
 def run_every_ab(args):
