@@ -921,27 +921,37 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
 // wrote through the cache; once the block outgrows the MALL those lines
 // only evict each other, and on the larger blocks every read-only round
 // does better streaming past it.
-constexpr int kNtLoadClasses = 3;
-std::atomic<uint32_t> g_defer_ntload[kNtLoadClasses] = { 0u, 0x41u, 0x5fu };
-// bit 7: the storing round's stores non-temporal too
+// Generalised (tools/defer_profile.py --defer-cache-ab): per dtype and size
+// class of every_cache_class (3 = the non-temporal form, from 2 GiB), bit NP
+// / bit kCapStore turns the matrix loads' policy over (cached <->
+// non-temporal) in that round, bit 7 the storing round's stores'.  The
+// non-temporal form and fp32 keep their own policies (see DESIGN.md
+// §Kernels, "the cache policy per launch").
+constexpr int kNtLoadClasses = 3;               // st_set_defer_ntload: fp64, cached
+constexpr int kDeferFlipClasses = 4;
+std::atomic<uint32_t> g_defer_flip[2][kDeferFlipClasses] = {
+  { 0u, 0u, 0u, 0u },            // fp32
+  { 0u, 0x41u, 0x5fu, 0u },      // fp64
+};
+// bit 7: the storing round's stores turned over too
 constexpr uint32_t kNtStoreBit = 7u;
 constexpr uint32_t kNtLoadMask = 0xdfu;
 
-// below 384 MiB, below 640 MiB, above
+// below 384 MiB, below 640 MiB, above (the cached fp64 classes of
+// st_set_defer_ntload)
 inline uint32_t
 defer_ntload_class(size_t bytes)
 {
   return bytes < ((size_t)384 << 20) ? 0u : bytes < ((size_t)640 << 20) ? 1u : 2u;
 }
 
-template <typename T, bool NT>
+template <typename T>
 inline uint32_t
-defer_ntload(uint32_t nrows, uint32_t ncols)
+defer_flip(uint32_t nrows, uint32_t ncols)
 {
-  if (NT || sizeof(T) != 8)
-    return 0u;
-  return g_defer_ntload[defer_ntload_class(block_bytes(nrows, ncols, sizeof(T)))]
-    .load(std::memory_order_relaxed);
+  return g_defer_flip[sizeof(T) == 8]
+                     [every_cache_class(block_bytes(nrows, ncols, sizeof(T)))]
+                       .load(std::memory_order_relaxed);
 }
 
 template <typename T, bool NT>
@@ -986,28 +996,24 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      uint32_t npend, bool store, bool flush,
                      hipStream_t stream)
 {
-  // cached fp64 blocks: non-temporal loads where g_defer_ntload says so
-  // (the other forms instantiate LNT = false only)
+  // the matrix loads' / stores' cache policy turned over where
+  // g_defer_flip says so (vector path only; kF64C: the cached fp64 form)
   constexpr bool kF64C = !NT && sizeof(T) == 8;
-  const uint32_t lnt = defer_ntload<T, NT>(nrows, ncols);
-#define ST_NPL(NPV, RV, STV, LNTV, PTV, LDS)                                   \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, LNTV>(                \
+  constexpr int kV = W > 1 ? 1 : 0;
+  const uint32_t fl = kV ? defer_flip<T>(nrows, ncols) : 0u;
+#define ST_NPL(NPV, RV, STV, FLV, PTV, LDS)                                    \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, false, (FLV) * kV>(   \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
 #define ST_NP(NPV, RV, PTV, LDS)                                               \
-  (((lnt >> (NPV)) & 1u) ? ST_NPL(NPV, RV, false, kF64C, PTV, LDS)             \
-                         : ST_NPL(NPV, RV, false, false, PTV, LDS))
-#define ST_NPLF(NPV, RV, LNTV, PTV, LDS)                                       \
-  (((lnt >> kNtStoreBit) & 1u)                                                 \
-     ? launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, true, LNTV,           \
-                               kF64C ? 2 : 0>(                                 \
-         a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0,     \
-         eps, k, max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS,    \
-         stream)                                                               \
-     : ST_NPL(NPV, RV, true, LNTV, PTV, LDS))
+  (((fl >> (NPV)) & 1u) ? ST_NPL(NPV, RV, false, 1, PTV, LDS)                  \
+                        : ST_NPL(NPV, RV, false, 0, PTV, LDS))
 #define ST_NPS(NPV, RV, PTV, LDS)                                              \
-  (((lnt >> kCapStore) & 1u) ? ST_NPLF(NPV, RV, kF64C, PTV, LDS)               \
-                             : ST_NPLF(NPV, RV, false, PTV, LDS))
+  (((fl >> kNtStoreBit) & 1u)                                                  \
+     ? (((fl >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, 3, PTV, LDS)          \
+                                 : ST_NPL(NPV, RV, true, 2, PTV, LDS))         \
+     : (((fl >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, 1, PTV, LDS)          \
+                                 : ST_NPL(NPV, RV, true, 0, PTV, LDS)))
   // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
   // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
   // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
@@ -1049,7 +1055,6 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   }
 #undef ST_NP
 #undef ST_NPS
-#undef ST_NPLF
 #undef ST_NPL
 }
 
@@ -1718,8 +1723,22 @@ st_set_defer_ntload(unsigned int size_class, unsigned int mask)
     st::set_error("st_set_defer_ntload: size class 0..2, mask of bits 0..4, 6 and 7");
     return -1;
   }
-  return (int)st::g_defer_ntload[size_class].exchange(mask,
-                                                      std::memory_order_relaxed);
+  return (int)st::g_defer_flip[1][size_class].exchange(mask,
+                                                       std::memory_order_relaxed);
+}
+
+int
+st_set_defer_cache(int dtype, unsigned int size_class, unsigned int mask)
+{
+  st::clear_error();
+  if ((dtype != 0 && dtype != 1) || size_class >= (unsigned)st::kDeferFlipClasses ||
+      (mask & ~st::kNtLoadMask) != 0) {
+    st::set_error("st_set_defer_cache: dtype 0/1, size class 0..3, mask of bits "
+                  "0..4, 6 and 7");
+    return -1;
+  }
+  return (int)st::g_defer_flip[dtype][size_class].exchange(mask,
+                                                           std::memory_order_relaxed);
 }
 
 int

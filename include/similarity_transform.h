@@ -350,6 +350,16 @@ int st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
  * on it.  Returns the previous mask, or -1 on bad arguments. */
 int st_set_defer_ntload(unsigned int size_class, unsigned int mask);
 
+/* The deferred rounds' cache policy in general: for dtype (0 = f32, 1 = f64)
+ * and size class (as st_set_every_cache: 0 below 384 MiB, 1 below 640 MiB,
+ * 2 below 2 GiB - the cached form - and 3 from 2 GiB - the non-temporal
+ * form), bit NP (0..4) of a read-only round with NP pending and bit 6 of a
+ * storing round turn that launch's matrix loads over (cached <->
+ * non-temporal), bit 7 the storing round's stores.  fp64 classes 0..2 are
+ * st_set_defer_ntload's masks.  For tuning tools; results do not depend on
+ * it.  Returns the previous mask, or -1 on bad arguments. */
+int st_set_defer_cache(int dtype, unsigned int size_class, unsigned int mask);
+
 /* The size class st_set_defer_ntload indexes for an nrows x ncols block
  * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
 int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);

@@ -194,6 +194,15 @@ def test_defer_ntload_setter():
         shipped.append(old)
         assert L.st_set_defer_ntload(cls, old) == 0x41
     assert shipped == [0, 0x41, 0x5f]
+    # the general form: fp64 classes 0..2 are the same masks
+    assert L.st_set_defer_cache(2, 0, 0) < 0 and L.st_set_defer_cache(1, 4, 0) < 0
+    assert L.st_set_defer_cache(0, 0, 0x20) < 0
+    assert L.st_set_defer_cache(1, 1, 0x41) == 0x41
+    shipped = [[L.st_set_defer_cache(d, c, 0) for c in range(4)] for d in (0, 1)]
+    for d in (0, 1):
+        for c in range(4):
+            assert L.st_set_defer_cache(d, c, shipped[d][c]) == 0
+    assert shipped == [[0, 0, 0, 0], [0, 0x41, 0x5f, 0]]
 
 
 def test_every_cache_setter():

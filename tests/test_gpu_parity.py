@@ -1204,6 +1204,33 @@ def test_deferred_ntload_does_not_change_results(solver, n):
         L.st_set_defer_ntload(cls, saved)
 
 
+@pytest.mark.parametrize("n,dtype", [(8192, "f32"), (16384, "f64"), (23200, "f32")])
+def test_deferred_cache_flip_does_not_change_results(solver, n, dtype):
+    """The deferred rounds' cache policy on the other forms
+    (st_set_defer_cache: cached fp32 blocks, and the non-temporal form from
+    2 GiB, whose loads / stores a mask turns cached) moves no result: λ, v,
+    iterations and the final matrix are bit-identical under every mask."""
+    L = _lib.load()
+    d = 1 if dtype == "f64" else 0
+    dt = torch.float64 if d else torch.float32
+    cls = L.st_every_cache_class(n, n, d)
+    assert cls == {8192: 0, 16384: 3, 23200: 3}[n]
+    base = dev.generate("random", n, dt, seed=12, device=DEV)
+    saved = L.st_set_defer_cache(d, cls, 0)
+    try:
+        out = []
+        for mask in (saved, 0x1f, 0x41, 0xdf):
+            assert L.st_set_defer_cache(d, cls, mask) >= 0
+            a = base.clone()
+            r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
+            out.append((r[0], r[2], r[1].cpu(), a))
+        for o in out[1:]:
+            assert o[0] == out[0][0] and o[1] == out[0][1]
+            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
+    finally:
+        L.st_set_defer_cache(d, cls, saved)
+
+
 @pytest.mark.parametrize("n", [4352, 8192, 10240])
 def test_every_cache_does_not_change_results(solver, n):
     """The every-round flat launch's cache policy (st_set_every_cache: the

@@ -106,6 +106,17 @@ def run_every_ab(args):
     return out
 
 
+def set_defer_cache(mask, n, elem, nrows=None):
+    """--defer-cache-ab: the deferred rounds' cache-policy flips for this
+    block's dtype and size class (st_set_defer_cache: bit NP 0..4 = read-only
+    round with NP pending, bit 6 = storing round's loads, bit 7 its stores)."""
+    from eigen_value_amd import _lib
+    L = _lib.load()
+    d = 1 if elem == 8 else 0
+    cls = L.st_every_cache_class(nrows or n, n, d)
+    _lib.check(L.st_set_defer_cache(d, cls, int(mask, 0)), "defer_cache")
+
+
 def run_caps_ab(args):
     """--caps-ab 'spec;spec;...' (st_set_defer_caps) or --ntload-ab
     'mask;mask;...' (st_set_defer_ntload): the same store cycles under each
@@ -125,6 +136,11 @@ def run_caps_ab(args):
 
         def apply(sp):
             set_ntload(sp, args.n, elem, sh.part.nrows)
+    elif args.defer_cache_ab:
+        what, specs = "defer-cache", args.defer_cache_ab.split(";")
+
+        def apply(sp):
+            set_defer_cache(sp, args.n, elem, sh.part.nrows)
     else:
         what, specs = "caps", args.caps_ab.split(";")
 
@@ -291,6 +307,8 @@ if __name__ == "__main__":
     p.add_argument("--caps-ab", help="A/B of caps specs separated by ';' (interleaved passes)")
     p.add_argument("--ntload-ab", help="A/B of non-temporal-load masks (cached fp64 blocks) "
                                        "separated by ';', e.g. '0;0x1;0x41'")
+    p.add_argument("--defer-cache-ab", help="A/B of deferred cache-policy masks "
+                   "(st_set_defer_cache, any dtype / size class) separated by ';'")
     p.add_argument("--every-ab", help="A/B of every-round cache policies (st_set_every_cache: "
                    "0 the form's, 1 / 2 / 3 loads / stores / both turned over) separated by ';'")
     p.add_argument("--steps", type=int, default=100, help="with --every-ab: rounds per pass")
@@ -302,7 +320,7 @@ if __name__ == "__main__":
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.caps_ab or a.ntload_ab or a.every_ab:
+    if a.caps_ab or a.ntload_ab or a.every_ab or a.defer_cache_ab:
         r = run_every_ab(a) if a.every_ab else run_caps_ab(a)
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)

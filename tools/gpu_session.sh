@@ -133,6 +133,16 @@ PY
         step "everyab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 100 --passes 5 --every-ab "$E_SPECS" --ab-json "$OUT/${RTAG}_everyab_${K}${N}_p${P}_$D.json"
         grep every-cache "$OUT/everyab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
       done ;;
+    dcab) # the deferred rounds' cache-policy flips on the other forms (st_set_defer_cache):
+          # the non-temporal form (loads / stores turned cached) and cached fp32 blocks
+      for W in ${DCAB_CASES:-random,32768,0,f64,6,0;0x1;0x3;0x1f;0x40;0x80 random,65536,8,f64,6,0;0x1;0x1f random,32768,0,f32,8,0;0x1;0x3;0x1f hilbert,8192,0,f32,60,0;0x1;0x41;0x5f random,12288,0,f32,30,0;0x1;0x41;0x5f random,16384,0,f32,20,0;0x1;0x41;0x5f}; do
+        IFS=, read -r K N P D C M <<< "$W"
+        step "dcab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --cycles $C --passes 5 --defer-cache-ab "$M" --ab-json "$OUT/${RTAG}_dcab_${K}${N}_p${P}_$D.json"
+        grep defer-cache "$OUT/dcab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
+      done ;;
+    ntab3) # the weak-scaled P = 4 block (4096 x 16384 fp64), whose deferred cycle trails 8192^2
+      step ntab3_hilbert16384_p4 300 python3 tools/defer_profile.py --kind hilbert --n 16384 --rank-block 4 --dtype f64 --cycles 40 --passes 7 --ntload-ab "0x41;0;0x1;0x5f;0x43;0x4f" --ab-json "$OUT/${RTAG}_ntab3_hilbert16384_p4_f64.json"
+      grep ntload "$OUT/ntab3_hilbert16384_p4.log" | tee -a "$OUT/session.log" ;;
     ntab2) # bit 7 of the cached fp64 deferred mask: the storing round's stores non-temporal
       for W in "hilbert 8192 0 0x41;0xc1;0x1;0x81" "hilbert 23040 8 0x41;0xc1" "hilbert 11648 2 0x41;0xc1" "random 10240 0 0x5f;0xdf" "random 12288 0 0x5f;0xdf" "random 6144 0 0;0x80;0x41;0xc1"; do
         set -- $W; K=$1; N=$2; P=$3; M=$4
@@ -140,7 +150,7 @@ PY
         grep ntload "$OUT/ntab2_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
       done ;;
     cachetests) # the bitwise tests of the cache-policy switches
-      step pytest_cache 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "every_cache or ntload" ;;
+      step pytest_cache 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "every_cache or ntload or cache_flip" ;;
     capsab4) # cached fp64 caps again, now that rounds load non-temporally (g_defer_ntload)
       C_SPECS="0,4,4,3,3,0,3;0,0,0,0,0,0,0;0,5,4,4,4,0,3;4,4,4,3,3,0,3;0,4,4,3,3,0,4;0,4,4,3,3,0,2;0,5,5,4,4,0,3"
       for W in "hilbert 8192 0" "hilbert 23040 8" "random 12288 0"; do
