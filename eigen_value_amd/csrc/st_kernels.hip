@@ -921,16 +921,23 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
 // wrote through the cache; once the block outgrows the MALL those lines
 // only evict each other, and on the larger blocks every read-only round
 // does better streaming past it.
-// Generalised (tools/defer_profile.py --defer-cache-ab): per dtype and size
-// class of every_cache_class (3 = the non-temporal form, from 2 GiB), bit NP
-// / bit kCapStore turns the matrix loads' policy over (cached <->
-// non-temporal) in that round, bit 7 the storing round's stores'.  The
-// non-temporal form and fp32 keep their own policies (see DESIGN.md
-// §Kernels, "the cache policy per launch").
+// Generalised (tools/defer_profile.py --defer-cache-ab, 5 interleaved
+// passes, two boxes, profiles/r03_dcab_*.json): per dtype and size class of
+// every_cache_class (3 = the non-temporal form, from 2 GiB), bit NP / bit
+// kCapStore turns the matrix loads' policy over (cached <-> non-temporal) in
+// that round, bit 7 the storing round's stores'.  Cached fp32 blocks from
+// 384 MiB gain like fp64 from non-temporal loads in the post-store and
+// storing rounds (0x41): 10240^2 0.0764 vs 0.0792 ms per round, 12288^2
+// 0.1091 / 0.1094 vs 0.1141 / 0.1146, 16384^2 0.1900 vs 0.1942, 20480^2
+// 0.3103 vs 0.3182; below (8192^2 fp32, the 5824 x 11648 block) every mask
+// loses.  On the non-temporal form every cached variant loses or ties
+// (32768^2 fp64 0x1 / 0x3 / 0x1f 1.499 / 1.523 / 1.617 vs 1.481 ms, 0x40 /
+// 0x80 1.478 / 1.485; fp32 0.739 - 0.758 vs 0.729; the P = 8 block 0.769 /
+// 0.827 vs 0.760), so it keeps both non-temporal.
 constexpr int kNtLoadClasses = 3;               // st_set_defer_ntload: fp64, cached
 constexpr int kDeferFlipClasses = 4;
 std::atomic<uint32_t> g_defer_flip[2][kDeferFlipClasses] = {
-  { 0u, 0u, 0u, 0u },            // fp32
+  { 0u, 0x41u, 0x41u, 0u },      // fp32
   { 0u, 0x41u, 0x5fu, 0u },      // fp64
 };
 // bit 7: the storing round's stores turned over too

@@ -202,7 +202,7 @@ def test_defer_ntload_setter():
     for d in (0, 1):
         for c in range(4):
             assert L.st_set_defer_cache(d, c, shipped[d][c]) == 0
-    assert shipped == [[0, 0, 0, 0], [0, 0x41, 0x5f, 0]]
+    assert shipped == [[0, 0x41, 0x41, 0], [0, 0x41, 0x5f, 0]]
 
 
 def test_every_cache_setter():
