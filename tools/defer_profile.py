@@ -30,6 +30,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
 
 
+# RELOAD_NOTE: the A/B modes regenerate A_0 before every pass.  A rank
+# block timed alone (--rank-block) holds the other ranks' row sums at 1.0,
+# so its off-block columns shrink by 1/s_r every round (Hilbert 5824 x 11648:
+# below 1e-300 after ~800 rounds, zeros after ~1300), and on blocks the
+# memory-side cache assists, zero-valued lines stream faster (8192^2 fp64:
+# the identity 0.1411 ms per round against 0.1533 for Hilbert or random
+# data, profiles/r03_data_dependence.log): passes over thousands of rounds
+# would drift.  Round 3's earlier A/B files (r03_everyab_*, r03_ntab*_*,
+# r03_capsab*_*) ran without the reload; their rank-block passes are
+# interleaved, so the comparisons hold, but late passes saw decayed data.
+
+
 def rounds_per_store(n, elem, f64):
     # st_defer_rounds: 6 on every block (round 2; round 1 took 3 or 4)
     return 6
@@ -91,6 +103,7 @@ def run_every_ab(args):
     for _ in range(args.passes):
         for sp in specs:
             set_every(sp, args.n, elem, sh.part.nrows)
+            sh.load(args.kind, seed=0)        # fresh A_0 per pass (see RELOAD_NOTE)
             res[sp].append(bench.timed_rounds(sh, args.steps, 4, torch, None, 1)[1])
     out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
                f" rank 0 of {args.rank_block}" if args.rank_block else ""),
@@ -152,7 +165,8 @@ def run_caps_ab(args):
     for _ in range(args.passes):
         for sp in specs:
             apply(sp)
-            res[sp].append(bench.timed_deferred(sh, args.cycles, 0, torch, None, 1)[1])
+            sh.load(args.kind, seed=0)        # fresh A_0 per pass (see RELOAD_NOTE)
+            res[sp].append(bench.timed_deferred(sh, args.cycles, 1, torch, None, 1)[1])
     out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
                f" rank 0 of {args.rank_block}" if args.rank_block else ""),
            "cycles": args.cycles, "passes": args.passes, "ms_per_round": {}}
@@ -291,7 +305,7 @@ def summarise_pmc(fetch, write, n, elem, m):
 if __name__ == "__main__":
     p = argparse.ArgumentParser()
     p.add_argument("--n", type=int, default=32768)
-    p.add_argument("--kind", default="random", choices=["hilbert", "random"])
+    p.add_argument("--kind", default="random", choices=["hilbert", "random", "identity"])
     p.add_argument("--cycles", type=int, default=8)
     p.add_argument("--dtype", default="f64", choices=["f64", "f32"])
     p.add_argument("--events", help="run mode: write the HIP-event figure here; summary "
