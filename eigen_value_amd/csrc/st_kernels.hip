@@ -135,16 +135,30 @@ round_shape(uint32_t nrows, uint32_t ncols, size_t elem)
   return { (size_t)ncols * elem <= ((size_t)96 << 10) ? 4 : 2, true, 256u };
 }
 
+// tools: st_set_mfree_shape (0 = the table below; 1 / 2 = cached, 2 / 4 rows;
+// 3 = non-temporal, 4 rows; grid 512)
+// The table: cached loads below 512 MiB, 4 rows per group up to 64 MiB and
+// again from 280 MiB (tools/defer_profile.py --mfree-ab, fresh A_0 per pass,
+// profiles/r03_mfab_*.json, ms per round, 2 rows vs 4): 6144^2 fp64 0.0462 vs
+// 0.0453, 7168^2 0.0674 vs 0.0637, 10240^2 fp32 0.0686 vs 0.0650, the P = 8
+// block 2880 x 23040 0.0928 vs 0.0867; below 280 MiB 2 rows (4608^2 fp64
+// 0.0255 vs 0.0264, 8192^2 fp32 0.0387 vs 0.0397); from 512 MiB
+// non-temporal 4 rows (8192^2 fp64 0.0810 against 0.0846 cached).
+std::atomic<uint32_t> g_mfree_shape{ 0u };
+
 inline Shape
 mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 {
   const size_t b = block_bytes(nrows, ncols, elem);
+  const uint32_t ov = g_mfree_shape.load(std::memory_order_relaxed);
+  if (ov != 0 && nrows >= 2 * kGridCap)
+    return { ov == 1 ? 2 : 4, ov == 3, 512u };
   if (nrows < 2 * kGridCap)
     return { 1, false, 1024u };
   if (b <= ((size_t)64 << 20))
     return { 4, false, 512u };
   if (b < ((size_t)512 << 20))
-    return { 2, false, 512u };
+    return { b >= ((size_t)280 << 20) ? 4 : 2, false, 512u };
   return { 4, true, 512u };
 }
 
@@ -1781,6 +1795,17 @@ st_set_every_tile(unsigned int size_class, unsigned int tile)
     return -1;
   }
   return (int)st::g_every_tile[size_class].exchange(tile, std::memory_order_relaxed);
+}
+
+int
+st_set_mfree_shape(unsigned int shape)
+{
+  st::clear_error();
+  if (shape > 3u) {
+    st::set_error("st_set_mfree_shape: shape 0..3");
+    return -1;
+  }
+  return (int)st::g_mfree_shape.exchange(shape, std::memory_order_relaxed);
 }
 
 int

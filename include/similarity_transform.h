@@ -380,6 +380,13 @@ int st_set_every_cache(unsigned int size_class, unsigned int policy);
  * depend on it.  Returns the previous value, or -1 on bad arguments. */
 int st_set_every_tile(unsigned int size_class, unsigned int tile);
 
+/* Launch shape of the matrix-free round (k_mfree) for every block of
+ * >= 2 x 256 row groups: 0 = the library's measured table, 1 / 2 = cached
+ * loads, 2 / 4 rows per group, 3 = non-temporal loads, 4 rows.  For tuning
+ * tools; results do not depend on it.  Returns the previous value, or -1
+ * on bad arguments. */
+int st_set_mfree_shape(unsigned int shape);
+
 /* The size class st_set_every_cache indexes for an nrows x ncols block
  * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
 int st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype);

@@ -1231,6 +1231,28 @@ def test_deferred_cache_flip_does_not_change_results(solver, n, dtype):
         L.st_set_defer_cache(d, cls, saved)
 
 
+@pytest.mark.parametrize("n,dtype", [(6144, "f64"), (4608, "f64"), (8192, "f32")])
+def test_mfree_shapes_do_not_change_results(solver, n, dtype):
+    """Every launch shape of the matrix-free round (st_set_mfree_shape:
+    cached 2 / 4 rows per group, non-temporal 4 rows, the table) gives the
+    same solve bit for bit (λ, v, iterations): the rows a workgroup takes
+    change no row's summation order."""
+    L = _lib.load()
+    dt = torch.float64 if dtype == "f64" else torch.float32
+    a = dev.generate("random", n, dt, seed=14, device=DEV)
+    saved = L.st_set_mfree_shape(0)
+    try:
+        out = []
+        for shape in (0, 1, 2, 3):
+            assert L.st_set_mfree_shape(shape) >= 0
+            r = solver.solve(a, matrix_free=True, eps=0.0, max_itr=7)
+            out.append((r[0], r[2], r[1].cpu()))
+        for o in out[1:]:
+            assert o[0] == out[0][0] and o[1] == out[0][1] and torch.equal(o[2], out[0][2])
+    finally:
+        L.st_set_mfree_shape(saved)
+
+
 @pytest.mark.parametrize("n", [4352, 8192, 10240])
 def test_every_cache_does_not_change_results(solver, n):
     """The every-round flat launch's cache policy (st_set_every_cache: the

@@ -84,6 +84,40 @@ def set_every(policy, n, elem, nrows=None):
     _lib.check(L.st_set_every_tile(cls, int(tile or "0", 0)), "every_tile")
 
 
+def run_mfree_ab(args):
+    """--mfree-ab 's;s;...': the matrix-free round (k_mfree) under each
+    launch shape (st_set_mfree_shape), --steps rounds per pass from a fresh
+    A_0, interleaved over --passes repeats; prints and returns the medians."""
+    import torch
+    import bench
+    from eigen_value_amd import _lib, sharded
+    L = _lib.load()
+    dt = torch.float64 if args.dtype == "f64" else torch.float32
+    rb = (args.rank_block, 0) if args.rank_block else None
+    sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb, matrix_free=True)
+    sh.load(args.kind, seed=0)
+    specs = args.mfree_ab.split(";")
+    res = {sp: [] for sp in specs}
+    _lib.check(L.st_set_mfree_shape(int(specs[0])), "mfree_shape")
+    bench.timed_rounds(sh, args.steps, 10, torch, None, 1)             # warm-up
+    for _ in range(args.passes):
+        for sp in specs:
+            _lib.check(L.st_set_mfree_shape(int(sp)), "mfree_shape")
+            res[sp].append(bench.timed_rounds(sh, args.steps, 4, torch, None, 1)[1])
+    out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
+               f" rank 0 of {args.rank_block}" if args.rank_block else ""),
+           "form": "matrix-free round (k_mfree)",
+           "steps": args.steps, "passes": args.passes, "ms_per_round": {}}
+    for sp in specs:
+        v = sorted(res[sp])
+        out["ms_per_round"][sp] = {"median": v[len(v) // 2], "min": v[0], "max": v[-1]}
+        print(f"{out['workload']} mfree-shape {sp:4s} median {v[len(v) // 2]:.5f} ms/round "
+              f"(min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
+    L.st_set_mfree_shape(0)
+    sh.close()
+    return out
+
+
 def run_every_ab(args):
     """--every-ab 'p;p;...': the every-round flat round (bench.py's timed
     step) under each cache policy, --steps rounds per pass, interleaved over
@@ -323,6 +357,8 @@ if __name__ == "__main__":
                                        "separated by ';', e.g. '0;0x1;0x41'")
     p.add_argument("--defer-cache-ab", help="A/B of deferred cache-policy masks "
                    "(st_set_defer_cache, any dtype / size class) separated by ';'")
+    p.add_argument("--mfree-ab", help="A/B of matrix-free launch shapes (st_set_mfree_shape: "
+                   "0 table, 1 / 2 cached 2 / 4 rows, 3 non-temporal 4 rows) separated by ';'")
     p.add_argument("--every-ab", help="A/B of every-round cache policies (st_set_every_cache: "
                    "0 the form's, 1 / 2 / 3 loads / stores / both turned over) separated by ';'")
     p.add_argument("--steps", type=int, default=100, help="with --every-ab: rounds per pass")
@@ -334,8 +370,9 @@ if __name__ == "__main__":
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.caps_ab or a.ntload_ab or a.every_ab or a.defer_cache_ab:
-        r = run_every_ab(a) if a.every_ab else run_caps_ab(a)
+    if a.caps_ab or a.ntload_ab or a.every_ab or a.defer_cache_ab or a.mfree_ab:
+        r = (run_mfree_ab(a) if a.mfree_ab else
+             run_every_ab(a) if a.every_ab else run_caps_ab(a))
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)
     elif a.trace or a.fetch:

@@ -140,6 +140,12 @@ PY
         step "dcab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --cycles $C --passes 5 --defer-cache-ab "$M" --ab-json "$OUT/${RTAG}_dcab_${K}${N}_p${P}_$D.json"
         grep defer-cache "$OUT/dcab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
       done ;;
+    mfab) # launch shapes of the matrix-free round (st_set_mfree_shape), fresh A_0 per run
+      for W in ${MFAB_CASES:-hilbert,8192,0,f64 hilbert,23040,8,f64 random,6144,0,f64 random,10240,0,f64 hilbert,8192,0,f32 random,12288,0,f32 random,16384,0,f32 random,32768,0,f64}; do
+        set -- ${W//,/ }; K=$1; N=$2; P=$3; D=$4
+        step "mfab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 100 --passes 5 --mfree-ab "${MFAB_SPECS:-0;1;2;3}" --ab-json "$OUT/${RTAG}_mfab_${K}${N}_p${P}_$D.json"
+        grep mfree-shape "$OUT/mfab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
+      done ;;
     ntab3) # the weak-scaled P = 4 block (4096 x 16384 fp64), whose deferred cycle trails 8192^2
       step ntab3_hilbert16384_p4 300 python3 tools/defer_profile.py --kind hilbert --n 16384 --rank-block 4 --dtype f64 --cycles 40 --passes 7 --ntload-ab "0x41;0;0x1;0x5f;0x43;0x4f" --ab-json "$OUT/${RTAG}_ntab3_hilbert16384_p4_f64.json"
       grep ntload "$OUT/ntab3_hilbert16384_p4.log" | tee -a "$OUT/session.log" ;;
@@ -150,7 +156,7 @@ PY
         grep ntload "$OUT/ntab2_${K}${N}_p$P.log" | tee -a "$OUT/session.log"
       done ;;
     cachetests) # the bitwise tests of the cache-policy switches
-      step pytest_cache 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "every_cache or ntload or cache_flip" ;;
+      step pytest_cache 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -rA --timeout 300 --timeout-method thread -k "every_cache or ntload or cache_flip or mfree_shapes" ;;
     capsab4) # cached fp64 caps again, now that rounds load non-temporally (g_defer_ntload)
       C_SPECS="0,4,4,3,3,0,3;0,0,0,0,0,0,0;0,5,4,4,4,0,3;4,4,4,3,3,0,3;0,4,4,3,3,0,4;0,4,4,3,3,0,2;0,5,5,4,4,0,3"
       for W in "hilbert 8192 0" "hilbert 23040 8" "random 12288 0"; do
