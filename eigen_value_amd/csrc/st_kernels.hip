@@ -35,15 +35,19 @@
 #ifndef ST_DEFER_STORE_R8_CACHED // 8 rows for the cached fp64 5-pending store
 #define ST_DEFER_STORE_R8_CACHED 1
 #endif
+#ifndef ST_FLAT_ALT // the flat launches' odd-round order (2 = reversed per XCD, 0 = none)
+#define ST_FLAT_ALT 2
+#endif
 #define ST_PROBES_DEFAULT                                                      \
   (ST_DPP_NOINIT == 1 && ST_ROW_VLOAD == 0 && ST_FLAT_UNMASKED == 1 &&         \
    ST_DEFER_STORE_NT == 0 && ST_EVERY_CACHED_R1 == 1 &&                        \
    ST_DEFER_R0_CACHED == 1 && ST_DEFER_PT0_CACHED == 4 &&                      \
-   ST_DEFER_STORE_R8_CACHED == 1)
+   ST_DEFER_STORE_R8_CACHED == 1 && ST_FLAT_ALT == 2)
 #ifndef ST_PROBES
 static_assert(ST_PROBES_DEFAULT,
               "A/B probe switch set in a library build (use -DST_PROBES=1)");
 #endif
+static_assert(ST_FLAT_ALT == 0 || ST_FLAT_ALT == 2, "ST_FLAT_ALT: 0 or 2");
 static_assert(ST_DEFER_R0_CACHED == 1 || ST_DEFER_R0_CACHED == 2 ||
                 ST_DEFER_R0_CACHED == 4,
               "ST_DEFER_R0_CACHED: 1, 2 or 4 rows");
@@ -174,7 +178,7 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 // 0.182; 6144^2 fp32 (144 MiB) 0.0472 vs 0.0478; at 128 MiB and below
 // k_round stays ahead: 4096^2 fp64 0.0412 vs 0.0426)
 constexpr int kFlatRows = 2; // rows per workgroup sharing a column piece
-constexpr int kFlatAlt = 2;  // odd rounds: pieces reversed per XCD (flat_reverse)
+constexpr int kFlatAlt = ST_FLAT_ALT; // odd rounds: pieces reversed per XCD (flat_reverse)
 // m_k / stop_k in k_flat's first row group (two launches per round) rather
 // than in a k_stats launch of their own (three)
 constexpr bool kFlatFusedStats = true;
@@ -1691,7 +1695,7 @@ st_probe_switches(void)
                    " ST_DEFER_R0_CACHED=" ST_STR(ST_DEFER_R0_CACHED)
                      " ST_DEFER_PT0_CACHED=" ST_STR(ST_DEFER_PT0_CACHED)
                        " ST_DEFER_STORE_R8_CACHED=" ST_STR(
-                         ST_DEFER_STORE_R8_CACHED);
+                         ST_DEFER_STORE_R8_CACHED) " ST_FLAT_ALT=" ST_STR(ST_FLAT_ALT);
 }
 
 unsigned int

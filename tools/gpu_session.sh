@@ -146,6 +146,17 @@ PY
         step "mfab_${K}${N}_p${P}_$D" 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 100 --passes 5 --mfree-ab "${MFAB_SPECS:-0;1;2;3}" --ab-json "$OUT/${RTAG}_mfab_${K}${N}_p${P}_$D.json"
         grep mfree-shape "$OUT/mfab_${K}${N}_p${P}_$D.log" | tee -a "$OUT/session.log"
       done ;;
+    libeab) # the every-round step (the bench's) under probe builds of the library, interleaved
+      for rep in 1 2 3; do
+        for V in base $LIBAB_VARIANTS; do
+          if [ "$V" = base ]; then LIBV=""; else LIBV="eigen_value_amd/lib/variants/$V/libsimilarity_transform.so"; fi
+          for W in ${LIBEAB_CASES:-hilbert,8192,0,f64}; do
+            set -- ${W//,/ }; K=$1; N=$2; P=$3; D=$4
+            EIGEN_VALUE_LIB=$LIBV step "libeab_${V}_${K}${N}_p${P}_${D}_$rep" 200 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 200 --passes 3 --every-ab 0
+            grep every-cache "$OUT/libeab_${V}_${K}${N}_p${P}_${D}_$rep.log" | sed "s/^/libeab $V /" | tee -a "$OUT/session.log"
+          done
+        done
+      done ;;
     ntab3) # the weak-scaled P = 4 block (4096 x 16384 fp64), whose deferred cycle trails 8192^2
       step ntab3_hilbert16384_p4 300 python3 tools/defer_profile.py --kind hilbert --n 16384 --rank-block 4 --dtype f64 --cycles 40 --passes 7 --ntload-ab "0x41;0;0x1;0x5f;0x43;0x4f" --ab-json "$OUT/${RTAG}_ntab3_hilbert16384_p4_f64.json"
       grep ntload "$OUT/ntab3_hilbert16384_p4.log" | tee -a "$OUT/session.log" ;;
