@@ -80,8 +80,9 @@ def set_every(policy, n, elem, nrows=None):
     L = _lib.load()
     cls = L.st_every_cache_class(nrows or n, n, 1 if elem == 8 else 0)
     pol, _, tile = policy.partition(":")      # "P" or "P:T" (T: st_set_every_tile)
-    _lib.check(L.st_set_every_cache(cls, int(pol, 0)), "every_cache")
-    _lib.check(L.st_set_every_tile(cls, int(tile or "0", 0)), "every_tile")
+    old_pol = _lib.check(L.st_set_every_cache(cls, int(pol, 0)), "every_cache")
+    old_tile = _lib.check(L.st_set_every_tile(cls, int(tile or "0", 0)), "every_tile")
+    return f"{old_pol}:{old_tile}"
 
 
 def run_mfree_ab(args):
@@ -132,7 +133,7 @@ def run_every_ab(args):
     sh.load(args.kind, seed=0)
     specs = args.every_ab.split(";")
     res = {sp: [] for sp in specs}
-    set_every(specs[0], args.n, elem, sh.part.nrows)
+    shipped = set_every(specs[0], args.n, elem, sh.part.nrows)
     bench.timed_rounds(sh, args.steps, 10, torch, None, 1)             # warm-up
     for _ in range(args.passes):
         for sp in specs:
@@ -148,7 +149,7 @@ def run_every_ab(args):
         out["ms_per_round"][sp] = {"median": v[len(v) // 2], "min": v[0], "max": v[-1]}
         print(f"{out['workload']} every-cache {sp:6s} median {v[len(v) // 2]:.5f} ms/round "
               f"(min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
-    set_every("0", args.n, elem, sh.part.nrows)
+    set_every(shipped, args.n, elem, sh.part.nrows)           # the library's own again
     sh.close()
     return out
 
