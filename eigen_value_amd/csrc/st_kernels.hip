@@ -314,6 +314,10 @@ flat_every_tile(uint32_t nrows, uint32_t ncols)
 // cache), and the non-temporal form keeps both non-temporal.
 constexpr int kEveryCacheClasses = 4;
 std::atomic<uint32_t> g_every_cache[kEveryCacheClasses] = { 2u, 2u, 0u, 0u };
+// workgroups per CU of the every-round launch per size class (0 = as many
+// as the registers allow; dynamic LDS the kernel does not use, as for the
+// deferred launches: defer_cap_lds), st_set_every_caps
+std::atomic<uint32_t> g_every_caps[kEveryCacheClasses] = { 0u, 0u, 0u, 0u };
 
 inline uint32_t
 every_cache_class(size_t bytes)
@@ -774,11 +778,14 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
       W == 1 ? 0u
              : g_every_cache[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))]
                  .load(std::memory_order_relaxed);
+    const uint32_t lds = defer_cap_lds(
+      g_every_caps[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))].load(
+        std::memory_order_relaxed));
 #define ST_EVERY(FL)                                                           \
   hipLaunchKernelGGL(                                                          \
     (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,         \
                  dev::kGatePlain, -1, U, false, -1, false, false, FL>),        \
-    fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,    \
+    fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v, nrows, ncols, ppr,  \
     row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
     constexpr int kV = W > 1 ? 1 : 0;
     switch (pol) {
@@ -1788,6 +1795,20 @@ st_set_every_cache(unsigned int size_class, unsigned int policy)
   }
   return (int)st::g_every_cache[size_class].exchange(policy,
                                                      std::memory_order_relaxed);
+}
+
+int
+st_set_every_caps(unsigned int size_class, unsigned int wg_per_cu)
+{
+  st::clear_error();
+  if (size_class >= (unsigned)st::kEveryCacheClasses || wg_per_cu == 1u ||
+      wg_per_cu > 32u) {
+    st::set_error("st_set_every_caps: size class 0..3, 0 (uncapped) or 2..32 "
+                  "workgroups per CU");
+    return -1;
+  }
+  return (int)st::g_every_caps[size_class].exchange(wg_per_cu,
+                                                    std::memory_order_relaxed);
 }
 
 int

@@ -374,6 +374,12 @@ int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);
  * or -1 on bad arguments. */
 int st_set_every_cache(unsigned int size_class, unsigned int policy);
 
+/* Workgroups per CU of the every-round flat launch per size class (the
+ * classes of st_set_every_cache; 0 = uncapped, else 2..32), held by dynamic
+ * LDS the kernel does not use.  For tuning tools; results do not depend on
+ * it.  Returns the previous value, or -1 on bad arguments. */
+int st_set_every_caps(unsigned int size_class, unsigned int wg_per_cu);
+
 /* Piece order of the every-round flat launch per size class (the classes of
  * st_set_every_cache): 0 = the library's measured table, 1 = row-major,
  * t > 1 = tiles of t row groups per piece.  For tuning tools; results do not

@@ -226,5 +226,9 @@ def test_every_cache_setter():
     assert shipped == [2, 2, 0, 0]
     assert L.st_set_every_tile(4, 0) < 0 and L.st_set_every_tile(0, 4097) < 0
     assert L.st_set_every_tile(1, 16) == 0 and L.st_set_every_tile(1, 0) == 16
+    assert L.st_set_every_caps(4, 0) < 0 and L.st_set_every_caps(0, 1) < 0
+    assert L.st_set_every_caps(0, 33) < 0
+    caps = [L.st_set_every_caps(c, 3) for c in range(4)]
+    assert [L.st_set_every_caps(c, caps[c]) for c in range(4)] == [3, 3, 3, 3]
     assert L.st_set_mfree_shape(4) < 0 and "st_set_mfree_shape" in _lib.last_error()
     assert L.st_set_mfree_shape(2) == 0 and L.st_set_mfree_shape(0) == 2
