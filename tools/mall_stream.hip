@@ -91,6 +91,79 @@ k_walk(double* a, double* part, unsigned nrows, unsigned ppr, unsigned pt,
   }
 }
 
+// the walk with k_flat's reduction after the loads: RED = 1 sums the lane's
+// values, reduces each wave (xor shuffles) and the workgroup's 4 waves
+// through LDS behind a barrier, one partial per piece (k_flat's shape);
+// RED = 2 stores one partial per wave, no barrier (k_flat's PW variant)
+template <int RED>
+__global__ __launch_bounds__(256) void
+k_walk_red(double* a, double* part, unsigned nrows, unsigned ppr, unsigned pt,
+           unsigned k, double f)
+{
+  const unsigned nb = gridDim.x;
+  unsigned b = blockIdx.x;
+  if (k & 1u) {
+    const unsigned g8 = nb & ~7u;
+    b = b < g8 ? g8 - 8 - (b & ~7u) + (b & 7u) : b;
+  }
+  const unsigned tile = b / (pt * ppr), t = b - tile * (pt * ppr);
+  const unsigned left = nrows - tile * pt, g = left < pt ? left : pt;
+  const unsigned p = t / g, r = tile * pt + (t - p * g);
+  d2* row = reinterpret_cast<d2*>(a + (size_t)r * ppr * 1024u + (size_t)p * 1024u);
+  d2 x0 = ld2<false>(row + threadIdx.x);
+  d2 x1 = ld2<false>(row + 256 + threadIdx.x);
+  x0 *= f;
+  x1 *= f;
+  st2<true>(row + threadIdx.x, x0);
+  st2<true>(row + 256 + threadIdx.x, x1);
+  double s = (x0.x + x0.y) + (x1.x + x1.y);
+  for (int o = 32; o >= 1; o >>= 1)
+    s += __shfl_xor(s, o);
+  const unsigned lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if constexpr (RED == 2) {
+    if (lane == 0)
+      part[(size_t)b * 4 + wave] = s;
+  } else {
+    __shared__ double red[4];
+    if (lane == 0)
+      red[wave] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      part[b] = (red[0] + red[1]) + (red[2] + red[3]);
+  }
+}
+
+template <int RED>
+static float
+run_red(double* a, double* part, unsigned nrows, unsigned ppr, unsigned pt,
+        unsigned lds)
+{
+  const unsigned grid = nrows * ppr;
+  hipEvent_t e0, e1;
+  HIPCHECK(hipEventCreate(&e0));
+  HIPCHECK(hipEventCreate(&e1));
+  for (unsigned k = 0; k < 16; k++)
+    hipLaunchKernelGGL((k_walk_red<RED>), dim3(grid), dim3(256), lds, 0, a, part,
+                       nrows, ppr, pt, k, 1.0);
+  std::vector<float> t;
+  for (int rep = 0; rep < 7; rep++) {
+    HIPCHECK(hipEventRecord(e0));
+    for (unsigned k = 0; k < 16; k++)
+      hipLaunchKernelGGL((k_walk_red<RED>), dim3(grid), dim3(256), lds, 0, a,
+                         part, nrows, ppr, pt, k, 1.0);
+    HIPCHECK(hipEventRecord(e1));
+    HIPCHECK(hipEventSynchronize(e1));
+    float ms = 0;
+    HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+    t.push_back(ms / 16);
+  }
+  HIPCHECK(hipGetLastError());
+  std::sort(t.begin(), t.end());
+  HIPCHECK(hipEventDestroy(e0));
+  HIPCHECK(hipEventDestroy(e1));
+  return t[t.size() / 2];
+}
+
 __global__ void
 k_fill(double* a, size_t n)
 {
@@ -151,7 +224,7 @@ main(int argc, char** argv)
     const unsigned ppr = nc / 1024;
     double *a = nullptr, *part = nullptr;
     HIPCHECK(hipMalloc(&a, n * sizeof(double)));
-    HIPCHECK(hipMalloc(&part, (size_t)nr * ppr * sizeof(double)));
+    HIPCHECK(hipMalloc(&part, (size_t)nr * ppr * 4 * sizeof(double)));
     hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, a, n);
     HIPCHECK(hipDeviceSynchronize());
     const double gb = n * sizeof(double) / 1e9;
@@ -176,6 +249,15 @@ main(int argc, char** argv)
       const float ms = run<false, true, true>(a, part, nr, ppr, pt, lds);
       std::printf("  rw cached / nt-store, %2u per CU %8.4f ms  %7.1f GB/s\n", cap, ms,
                   2 * gb / (ms * 1e-3));
+      std::fflush(stdout);
+    }
+    // + the reduction (cached loads, non-temporal stores, as k_flat ships)
+    for (unsigned cap : { 0u, 3u, 4u, 6u }) {
+      const unsigned lds = cap ? (160u << 10) / cap - 2048u : 0u;
+      const float m1 = run_red<1>(a, part, nr, ppr, pt, lds);
+      const float m2 = run_red<2>(a, part, nr, ppr, pt, lds);
+      std::printf("  + reduction, %2u per CU: one partial per piece %8.4f ms, per wave "
+                  "%8.4f ms\n", cap, m1, m2);
       std::fflush(stdout);
     }
     HIPCHECK(hipFree(a));
