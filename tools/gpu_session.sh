@@ -152,7 +152,7 @@ PY
           if [ "$V" = base ]; then LIBV=""; else LIBV="eigen_value_amd/lib/variants/$V/libsimilarity_transform.so"; fi
           for W in ${LIBEAB_CASES:-hilbert,8192,0,f64}; do
             set -- ${W//,/ }; K=$1; N=$2; P=$3; D=$4
-            EIGEN_VALUE_LIB=$LIBV step "libeab_${V}_${K}${N}_p${P}_${D}_$rep" 200 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 200 --passes 3 --every-ab 0
+            EIGEN_VALUE_LIB=$LIBV step "libeab_${V}_${K}${N}_p${P}_${D}_$rep" 200 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype $D --steps 200 --passes 3 --every-ab "${LIBEAB_SPECS:-2}"
             grep every-cache "$OUT/libeab_${V}_${K}${N}_p${P}_${D}_$rep.log" | sed "s/^/libeab $V /" | tee -a "$OUT/session.log"
           done
         done
