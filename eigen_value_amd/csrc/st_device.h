@@ -1381,6 +1381,20 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
 }
 
+// The solve loops' per-batch look at the state: one wave copies the 64 B
+// st_state into the caller's pinned, host-coherent slot with vector stores
+// (16 lanes, one word each), in stream order behind the batch's rounds.  It
+// replaces a device-to-host copy on the stream, a blit launch whose own
+// dispatch gaps cost ~20 us per batch (rocprofv3 trace of the whole solves,
+// profiles/r03_state_mirror_*.log).
+__global__ __launch_bounds__(64) void
+k_state_mirror(const uint32_t* __restrict__ d, uint32_t* h)
+{
+  const uint32_t i = threadIdx.x;
+  if (i < (uint32_t)(sizeof(st_state) / 4))
+    __hip_atomic_store(&h[i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // k_parts with one THREAD per row (sweep variant): the row's partials in
 // four interleaved running sums, ((a0 + a1) + (a2 + a3)), no wave reduction
 template <typename T, int BLK = kBlock>

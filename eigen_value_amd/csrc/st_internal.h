@@ -107,6 +107,11 @@ int launch_mfree_flat(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
 template <typename T>
 int launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
                     uint32_t semantics, st_state* st, hipStream_t stream);
+// st_state -> pinned host-coherent memory, in stream order (the solve loops'
+// per-batch flag read)
+int launch_state_mirror(const st_state* d_state, st_state* h_state,
+                        hipStream_t stream);
+
 template <typename T>
 int launch_fill(T* x, uint64_t count, T value, hipStream_t stream);
 // the whole solve in one workgroup (k_solve_small): v = 1, s_0, every round,

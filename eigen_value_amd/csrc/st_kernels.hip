@@ -1381,6 +1381,16 @@ launch_epilogue(const T* s, T* v, uint32_t n, T eps, uint32_t max_itr,
   return check_launch("epilogue");
 }
 
+int
+launch_state_mirror(const st_state* d_state, st_state* h_state, hipStream_t stream)
+{
+  ST_REQUIRE(d_state && h_state, "state_mirror: null pointer");
+  hipLaunchKernelGGL(dev::k_state_mirror, dim3(1), dim3(64), 0, stream,
+                     reinterpret_cast<const uint32_t*>(d_state),
+                     reinterpret_cast<uint32_t*>(h_state));
+  return check_launch("state_mirror");
+}
+
 template <typename T>
 int
 launch_fill(T* x, uint64_t count, T value, hipStream_t stream)

@@ -220,7 +220,8 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
       return -1;
   }
   ST_CHECK(hipSetDevice(M.sh[0].dev));
-  ST_CHECK(hipHostMalloc(&M.h_state, 2 * sizeof(st_state), hipHostMallocDefault));
+  ST_CHECK(hipHostMalloc(&M.h_state, 2 * sizeof(st_state),
+                         hipHostMallocCoherent | hipHostMallocMapped));
   ST_CHECK(hipEventCreateWithFlags(&M.ev[0], hipEventDisableTiming));
   ST_CHECK(hipEventCreateWithFlags(&M.ev[1], hipEventDisableTiming));
   if (batch == 0) // as st_solve.hip: flat rounds are checked every 2 rounds
@@ -307,8 +308,8 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
     const int slot = batch_no & 1;
     Shard<T>& d0 = M.sh[0];
     ST_CHECK(hipSetDevice(d0.dev));
-    ST_CHECK(hipMemcpyAsync(&M.h_state[slot], d0.state, sizeof(st_state),
-                            hipMemcpyDeviceToHost, d0.stream));
+    if (launch_state_mirror(d0.state, &M.h_state[slot], d0.stream))
+      return -1;
     ST_CHECK(hipEventRecord(M.ev[slot], d0.stream));
     if (batch_no > 0) {
       ST_CHECK(hipEventSynchronize(M.ev[slot ^ 1]));

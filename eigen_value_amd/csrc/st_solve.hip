@@ -323,8 +323,8 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     }
     enqueued += b;
     const int slot = batch_no & 1;
-    ST_CHECK(hipMemcpyAsync(&c->h_state[slot], c->d_state, sizeof(st_state),
-                            hipMemcpyDeviceToHost, s));
+    if (launch_state_mirror(c->d_state, &c->h_state[slot], s))
+      return -1;
     ST_CHECK(hipEventRecord(c->ev_flag[slot], s));
     // wait for the previous batch's flag while this batch runs
     if (batch_no > 0) {
@@ -494,7 +494,7 @@ make_queue(void** wq)
               hipSuccess &&
             hipMalloc(&c->d_state, sizeof(st_state)) == hipSuccess &&
             hipHostMalloc(&c->h_state, 2 * sizeof(st_state),
-                          hipHostMallocDefault) == hipSuccess &&
+                          hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess &&
             hipEventCreateWithFlags(&c->ev_flag[0], hipEventDisableTiming) ==
               hipSuccess &&
             hipEventCreateWithFlags(&c->ev_flag[1], hipEventDisableTiming) ==
