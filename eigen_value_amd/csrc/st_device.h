@@ -966,7 +966,7 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool MF = false, bool LNT = false, int FLIP = 0>
+          int DS = -1, bool MF = false, int FLIP = 0>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
@@ -1000,11 +1000,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
   // compile time (1 / 0; the library's launches), or -1 = pend.store at
   // run time (the sweep tools)
-  // LNT: matrix loads non-temporal on a cached-form launch (the piece size
-  // stays the form's; ST_DEFER_NTLOAD_CACHED)
-  // FLIP: the every-round launch's cache policy (st_set_every_cache): bit 0
-  // turns the matrix loads' policy over (cached <-> non-temporal), bit 1
-  // the stores'; the shapes stay the form's
+  // FLIP: the launch's cache policy (g_every_cache / g_defer_flip in
+  // st_kernels.hip): bit 0 turns the matrix loads' policy over (cached <->
+  // non-temporal), bit 1 the stores'; the shapes stay the form's
   // MF: the matrix-free round's sweep (launch k >= 1 of k_mfree's scheme,
   // with FS): `a` is A_0 (read only), `v` is v_{k-2}; each piece's partial
   // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
@@ -1101,7 +1099,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // the deferred rounds' stores (probe switch ST_DEFER_STORE_NT: non-temporal
   // on cached blocks too)
   constexpr bool NTS = (NT || (NP >= 0 && ST_DEFER_STORE_NT)) != ((FLIP & 2) != 0);
-  constexpr bool NTL = (NT || LNT) != ((FLIP & 1) != 0);
+  constexpr bool NTL = NT != ((FLIP & 1) != 0);
   uint32_t cl[U]; // the column each lane loads
 #pragma unroll
   for (int u = 0; u < U; u++)

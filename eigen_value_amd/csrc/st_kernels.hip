@@ -784,7 +784,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
 #define ST_EVERY(FL)                                                           \
   hipLaunchKernelGGL(                                                          \
     (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,         \
-                 dev::kGatePlain, -1, U, false, -1, false, false, FL>),        \
+                 dev::kGatePlain, -1, U, false, -1, false, FL>),               \
     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v, nrows, ncols, ppr,  \
     row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
     constexpr int kV = W > 1 ? 1 : 0;
@@ -866,7 +866,7 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // 0.053 vs 0.078.  Longer groups lose: the pending scales' loads and
 // registers outgrow the bytes saved.
 template <typename T, int W, int ORDER, bool NT, int NP, int R, bool STORE,
-          bool LNT, int FL = 0>
+          int FL = 0>
 void
 launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                         T* inv_next, T* part, T* v, uint32_t nrows,
@@ -891,7 +891,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   // workgroups per CU (see launch_flat_deferred)
   hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
                                   kBlock, 0, dev::kGatePlain, NP, U, false,
-                                  STORE ? 1 : 0, false, LNT, FL>),
+                                  STORE ? 1 : 0, false, FL>),
                      fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
                      0u, 0u, 0u, pd, fg.gx2);
@@ -1034,7 +1034,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr int kV = W > 1 ? 1 : 0;
   const uint32_t fl = kV ? defer_flip<T>(nrows, ncols) : 0u;
 #define ST_NPL(NPV, RV, STV, FLV, PTV, LDS)                                    \
-  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, false, (FLV) * kV>(   \
+  launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, (FLV) * kV>(          \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
 #define ST_NP(NPV, RV, PTV, LDS)                                               \
