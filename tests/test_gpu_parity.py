@@ -1266,8 +1266,12 @@ def test_every_cache_does_not_change_results(solver, n):
     saved = L.st_set_every_cache(cls, 0)
     try:
         out = []
-        for pol in (saved, 0, 1, 2, 3):
+        # (policy, piece tile, workgroups per CU): st_set_every_tile and
+        # st_set_every_caps are for tools, and move no result either
+        for pol, tile, cap in ((saved, 0, 0), (0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0),
+                               (saved, 1, 0), (saved, 16, 3)):
             assert L.st_set_every_cache(cls, pol) >= 0
+            assert L.st_set_every_tile(cls, tile) >= 0 and L.st_set_every_caps(cls, cap) >= 0
             a = base.clone()
             r = solver.solve(a, inplace=True, eps=0.0, max_itr=7, write_every_round=True)
             out.append((r[0], r[2], r[1].cpu(), a))
@@ -1276,6 +1280,8 @@ def test_every_cache_does_not_change_results(solver, n):
             assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
     finally:
         L.st_set_every_cache(cls, saved)
+        L.st_set_every_tile(cls, 0)
+        L.st_set_every_caps(cls, 0)
 
 
 @pytest.mark.parametrize("limit", [8, 1000, 4096])
