@@ -187,8 +187,6 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_set_every_caps.argtypes = [u32, u32]
     L.st_set_every_caps.restype = i32
     L.st_set_defer_cache.argtypes = [i32, u32, u32]
-    L.st_set_flat_fold.argtypes = [u32]
-    L.st_set_flat_fold.restype = i32
     L.st_set_mfree_shape.argtypes = [u32]
     L.st_set_mfree_shape.restype = i32
     L.st_set_defer_cache.restype = i32

@@ -966,10 +966,10 @@ struct FlatPending
 template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
           bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
           int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool MF = false, int FLIP = 0, int FV = 1>
+          int DS = -1, bool MF = false, int FLIP = 0>
 __global__ __launch_bounds__(BLK) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
-       T* __restrict__ v, uint32_t nrows_b, uint32_t ncols_b, uint32_t ppr_b,
+       T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
@@ -1009,23 +1009,6 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // group folds round k-1's stats, nothing is stored; k_mparts finishes
   // s_k and v_{k-1}
   static_assert(!MF || (FS && NP < 0 && SPLIT == 0), "MF: the fused-stats unsplit round");
-  // FV (folded rows, long-row blocks): the block's nrows_b x ncols_b rows
-  // are walked as FV * nrows_b virtual rows of ncols_b / FV columns - the
-  // same bytes in the same row-major order, so a virtual row's address is
-  // its physical one and its piece p is the physical row's piece
-  // h * ppr_b / FV + p (h = which FV-th of the row): the partials land
-  // where the unfolded walk puts them, each summed by the same tree.  What
-  // the fold changes is which addresses a workgroup and its neighbours load
-  // together: R virtual rows of one physical row, ncols_b / FV elements
-  // apart, instead of R rows ncols_b apart (8192 x 65536 fp64 streams at
-  // 6.38 TB/s, the same bytes as 16384 x 32768 at 6.56, see
-  // flat_fold_rows in st_kernels.hip).  Column scales then differ between
-  // the FV virtual rows of a physical row (one set per h), the row scales
-  // are the physical row's.  The launcher guarantees ncols_b % (FV * PWC) ==
-  // 0 and R % FV == 0, so no piece straddles two virtual rows.
-  static_assert(FV == 1 || (SPLIT == 0 && !MF && !FOLD && !PW && R % FV == 0),
-                "FV: the unsplit row-group form");
-  const uint32_t nrows = nrows_b * FV, ncols = ncols_b / FV, ppr = ppr_b / FV;
   // the matrix-free launch k evaluates round k - 1 (gated once end <= k - 1)
   const uint32_t kr = MF ? k - 1 : k;
   if constexpr (GATE != kGateSpec) {
@@ -1143,33 +1126,29 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
   // the piece's column scales, issued with the matrix loads (the stats of
   // the first row group read them too)
-  V sc[FV][U]; // [h][u]: virtual row r0 + j takes sc[j % FV] (r0 % FV == 0)
+  V sc[U];
 #pragma unroll
-  for (int h = 0; h < FV; h++)
-#pragma unroll
-    for (int u = 0; u < U; u++)
-      if (UM || in_cols[u])
-        sc[h][u] = *reinterpret_cast<const V*>(s_cur + h * ncols + cl[u]);
+  for (int u = 0; u < U; u++)
+    if (UM || in_cols[u])
+      sc[u] = *reinterpret_cast<const V*>(s_cur + cl[u]);
   // matrix-free: x = v_{k-2} ∘ s_{k-1} for the piece's columns
   V xs[MF ? U : 1];
   if constexpr (MF) {
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (in_cols[u])
-        xs[u] = *reinterpret_cast<const V*>(v + cl[u]) * sc[0][u];
+        xs[u] = *reinterpret_cast<const V*>(v + cl[u]) * sc[u];
   }
   // deferred writes: the pending rounds' column scales
-  V sp_c[NP > 0 ? NP : 1][FV][U];
+  V sp_c[NP > 0 ? NP : 1][U];
   T sp_r[NP > 0 ? NP : 1][R]; // 1 / s_i[r]
   if constexpr (NP > 0) {
 #pragma unroll
     for (int i = 0; i < NP; i++) {
 #pragma unroll
-      for (int h = 0; h < FV; h++)
-#pragma unroll
-        for (int u = 0; u < U; u++)
-          if (UM || in_cols[u])
-            sp_c[i][h][u] = *reinterpret_cast<const V*>(pend.s[i] + h * ncols + cl[u]);
+      for (int u = 0; u < U; u++)
+        if (UM || in_cols[u])
+          sp_c[i][u] = *reinterpret_cast<const V*>(pend.s[i] + cl[u]);
     }
   }
   // then the row scales (vector loads, ld_row): s_k[r], or with deferred
@@ -1189,25 +1168,25 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   if (kMergeRows && r0 + R <= nrows) { // uniform
 #pragma unroll
     for (int j = 0; j < R; j++)
-      sr[j] = ld_row(rs + row0 + (r0 + j) / FV);
+      sr[j] = ld_row(rs + row0 + r0 + j);
     if constexpr (NP > 0) {
 #pragma unroll
       for (int i = 0; i < NP; i++) {
 #pragma unroll
         for (int j = 0; j < R; j++)
-          sp_r[i][j] = ld_row(pend.inv[i] + row0 + (r0 + j) / FV);
+          sp_r[i][j] = ld_row(pend.inv[i] + row0 + r0 + j);
       }
     }
   } else {
 #pragma unroll
     for (int j = 0; j < R; j++)
-      sr[j] = r0 + j < nrows ? ld_row(rs + row0 + (r0 + j) / FV) : (T)1;
+      sr[j] = r0 + j < nrows ? ld_row(rs + row0 + r0 + j) : (T)1;
     if constexpr (NP > 0) {
 #pragma unroll
       for (int i = 0; i < NP; i++) {
 #pragma unroll
         for (int j = 0; j < R; j++)
-          sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + (r0 + j) / FV) : (T)1;
+          sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
       }
     }
   }
@@ -1221,12 +1200,10 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       T mx = (T)0;
       int ok = 1;
 #pragma unroll
-      for (int h = 0; h < FV; h++)
-#pragma unroll
-        for (int u = 0; u < U; u++)
-          if (in_cols[u])
-            stats_at<T, W>(s_cur, sc[h][u], (h * ncols + c0 + u * BLK * W) / W, ncols_b,
-                           semantics == ST_SEM_SYCL, eps, mx, ok);
+      for (int u = 0; u < U; u++)
+        if (in_cols[u])
+          stats_at<T, W>(s_cur, sc[u], (c0 + u * BLK * W) / W, ncols,
+                         semantics == ST_SEM_SYCL, eps, mx, ok);
       int fail = ok ? 0 : 1;
       mx = wave_max(mx);
       if ((threadIdx.x & 63) == 0)
@@ -1252,9 +1229,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         for (int j = 0; j < R; j++) {
           const T inv = sp_r[i][j];
           if constexpr (ORDER == 0)
-            x[u][j] = x[u][j] * (inv * sp_c[i][j % FV][u]);
+            x[u][j] = x[u][j] * (inv * sp_c[i][u]);
           else
-            x[u][j] = (inv * x[u][j]) * sp_c[i][j % FV][u];
+            x[u][j] = (inv * x[u][j]) * sp_c[i][u];
         }
       }
     }
@@ -1264,9 +1241,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
       V y;
       if constexpr (ORDER == 0)
-        y = x[u][j] * (inv * sc[j % FV][u]); // cpp:324-325
+        y = x[u][j] * (inv * sc[u]); // cpp:324-325
       else
-        y = (inv * x[u][j]) * sc[j % FV][u]; // main.py:13-16
+        y = (inv * x[u][j]) * sc[u]; // main.py:13-16
       if (do_store && in_cols[u] && r0 + j < nrows)
         st<V, NTS>(reinterpret_cast<V*>(wp), y);
       wp += ncols;
@@ -1287,9 +1264,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
           if (r0 + j < nrows) {
             const T inv = sp_r[i][j];
             if constexpr (ORDER == 0)
-              x[u][j] = x[u][j] * (inv * sp_c[i][j % FV][u]);
+              x[u][j] = x[u][j] * (inv * sp_c[i][u]);
             else
-              x[u][j] = (inv * x[u][j]) * sp_c[i][j % FV][u];
+              x[u][j] = (inv * x[u][j]) * sp_c[i][u];
           }
         }
       }
@@ -1311,9 +1288,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
         V y;
         if constexpr (ORDER == 0)
-          y = x[u][j] * (inv * sc[j % FV][u]); // cpp:324-325
+          y = x[u][j] * (inv * sc[u]); // cpp:324-325
         else
-          y = (inv * x[u][j]) * sc[j % FV][u]; // main.py:13-16
+          y = (inv * x[u][j]) * sc[u]; // main.py:13-16
         if (do_store)
           st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
                     y);
@@ -1321,11 +1298,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       }
     }
   }
-  if (!FS && SPLIT == 0 && p == 0 && threadIdx.x < R / FV &&
-      r0 / FV + threadIdx.x < nrows_b) {
-    // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats (folded: the
-    // workgroup of virtual piece 0 holds piece 0 of R / FV physical rows)
-    const uint32_t r = row0 + r0 / FV + threadIdx.x;
+  if (!FS && SPLIT == 0 && p == 0 && threadIdx.x < R && r0 + threadIdx.x < nrows) {
+    // v[r] *= s_k[r] / m_k (cpp:260), m_k from k_stats
+    const uint32_t r = row0 + r0 + threadIdx.x;
     const T m = (T)state->max;
     v[r] = v[r] * (s_cur[r] / m);
   }

@@ -319,36 +319,6 @@ std::atomic<uint32_t> g_every_cache[kEveryCacheClasses] = { 2u, 2u, 0u, 0u };
 // deferred launches: defer_cap_lds), st_set_every_caps
 std::atomic<uint32_t> g_every_caps[kEveryCacheClasses] = { 0u, 0u, 0u, 0u };
 
-// Folded rows (k_flat FV = 2) for long-row blocks: a non-temporal block
-// whose rows hold >= 512 KiB (fp64 from 65536 columns - configs[3] and its
-// rank blocks) is walked as twice as many rows of half the length, the same
-// bytes in the same order with every partial where the unfolded walk puts
-// it (results bitwise equal, test_flat_fold_bitwise).  Single every-round
-// launches (tools/flat_map_sweep FMS_EVERY=1, profiles/r03_shape_walk.log):
-// 8192 x 65536 fp64 1.3458 ms (6.38 TB/s) against 1.3102 ms (6.56 TB/s) for
-// the same 4 GiB laid out 16384 x 32768 - the long rows' 2-3 % of round 2's
-// verdict is the walk of rows 512 KiB apart, not the bytes.  Bit 0 folds the
-// every-round launch, bit 1 the deferred rounds' (st_set_flat_fold, for
-// tools; results do not depend on it).
-std::atomic<uint32_t> g_flat_fold{ 3u };
-
-template <typename T, int W, int U, bool NT>
-inline bool
-flat_fold_rows(uint32_t ncols, uint32_t bit)
-{
-  constexpr uint32_t kPwc = (uint32_t)kBlock * W * U;
-  return NT && W > 1 && (g_flat_fold.load(std::memory_order_relaxed) & bit) != 0 &&
-         (size_t)ncols * sizeof(T) >= ((size_t)512 << 10) && ncols % (2 * kPwc) == 0;
-}
-
-// k_flat's grid over nrows x ncols (ppr pieces of a row) in rows of R,
-// folded by fv
-inline uint32_t
-flat_fold_grid(uint32_t nrows, uint32_t ppr, uint32_t r, uint32_t fv)
-{
-  return (nrows * fv + r - 1) / r * (ppr / fv);
-}
-
 inline uint32_t
 every_cache_class(size_t bytes)
 {
@@ -795,8 +765,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
   // rows per workgroup: 2, one on cached fp64 blocks (below)
   constexpr int R = kFlatEveryRows<T, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
-  const bool fold = R % 2 == 0 && flat_fold_rows<T, W, U, NT>(ncols, 1u);
-  const uint32_t grid = flat_fold_grid(nrows, ppr, R, fold ? 2u : 1u);
+  const uint32_t grid = (nrows + R - 1) / R * ppr;
   const uint32_t pgrid = (nrows + dev::kWaves - 1) / dev::kWaves;
   const FlatGrid fg = flat_grid(grid);
   dev::FlatPending<T, -1> pe{};
@@ -812,28 +781,13 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     const uint32_t lds = defer_cap_lds(
       g_every_caps[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))].load(
         std::memory_order_relaxed));
-#define ST_EVERY_FV(FL, FV)                                                    \
+#define ST_EVERY(FL)                                                           \
   hipLaunchKernelGGL(                                                          \
     (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,         \
-                 dev::kGatePlain, -1, U, false, -1, false, FL, FV>),           \
+                 dev::kGatePlain, -1, U, false, -1, false, FL>),               \
     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v, nrows, ncols, ppr,  \
     row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
-#define ST_EVERY(FL) ST_EVERY_FV(FL, 1)
     constexpr int kV = W > 1 ? 1 : 0;
-    if constexpr (NT && W > 1 && R % 2 == 0) {
-      // folded long rows (flat_fold_rows): the non-temporal form's own policy
-      // or a tool's override, as below
-      if (fold) {
-        switch (pol) {
-          case 1u: ST_EVERY_FV(1, 2); break;
-          case 2u: ST_EVERY_FV(2, 2); break;
-          case 3u: ST_EVERY_FV(3, 2); break;
-          default: ST_EVERY_FV(0, 2); break;
-        }
-        launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr, stream);
-        return;
-      }
-    }
     switch (pol) {
       case 1u: ST_EVERY(kV); break;
       case 2u: ST_EVERY(2 * kV); break;
@@ -841,7 +795,6 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
       default: ST_EVERY(0); break;
     }
 #undef ST_EVERY
-#undef ST_EVERY_FV
     launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, nullptr, stream);
   } else {
     const uint32_t sgrid =
@@ -924,8 +877,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 {
   constexpr int U = kFlatU<T, W, NT>;
   const uint32_t ppr = flat_pieces(ncols, W * U);
-  const bool fold = R % 2 == 0 && flat_fold_rows<T, W, U, NT>(ncols, 2u);
-  const uint32_t grid = flat_fold_grid(nrows, ppr, R, fold ? 2u : 1u);
+  const uint32_t grid = (nrows + R - 1) / R * ppr;
   dev::FlatPending<T, NP> pd{};
   for (int i = 0; i < NP; i++) {
     pd.s[i] = pend_s[i];
@@ -937,23 +889,12 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   const FlatGrid fg = flat_grid(grid);
   // lds: dynamic LDS the kernel does not use, reserved only to cap the
   // workgroups per CU (see launch_flat_deferred)
-#define ST_DEFER_FV(FV)                                                        \
-  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,   \
-                                  kBlock, 0, dev::kGatePlain, NP, U, false,    \
-                                  STORE ? 1 : 0, false, FL, FV>),              \
-                     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,    \
-                     nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,  \
-                     0u, 0u, 0u, pd, fg.gx2)
-  bool done = false;
-  if constexpr (NT && W > 1 && R % 2 == 0) {
-    if (fold) { // folded long rows (flat_fold_rows)
-      ST_DEFER_FV(2);
-      done = true;
-    }
-  }
-  if (!done)
-    ST_DEFER_FV(1);
-#undef ST_DEFER_FV
+  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
+                                  kBlock, 0, dev::kGatePlain, NP, U, false,
+                                  STORE ? 1 : 0, false, FL>),
+                     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
+                     nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
+                     0u, 0u, 0u, pd, fg.gx2);
   if (!flush) // a flush only stores the matrix: s, v and the state stand
     launch_parts<T>(part, s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next, stream);
 }
@@ -1889,17 +1830,6 @@ st_set_every_tile(unsigned int size_class, unsigned int tile)
     return -1;
   }
   return (int)st::g_every_tile[size_class].exchange(tile, std::memory_order_relaxed);
-}
-
-int
-st_set_flat_fold(unsigned int mask)
-{
-  st::clear_error();
-  if (mask > 3u) {
-    st::set_error("st_set_flat_fold: mask 0..3 (bit 0 every-round, bit 1 deferred)");
-    return -1;
-  }
-  return (int)st::g_flat_fold.exchange(mask, std::memory_order_relaxed);
 }
 
 int

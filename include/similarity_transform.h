@@ -386,14 +386,6 @@ int st_set_every_caps(unsigned int size_class, unsigned int wg_per_cu);
  * depend on it.  Returns the previous value, or -1 on bad arguments. */
 int st_set_every_tile(unsigned int size_class, unsigned int tile);
 
-/* Folded rows of the flat round on non-temporal blocks with rows of
- * >= 512 KiB (fp64 from 65536 columns): each row walked as two of half the
- * length, the same bytes and partials ("folded long
- * rows").  Bit 0 folds the every-round launch, bit 1 the deferred rounds';
- * default 3.  For tuning tools; results do not depend on it.  Returns the
- * previous mask, or -1 on bad arguments. */
-int st_set_flat_fold(unsigned int mask);
-
 /* Launch shape of the matrix-free round (k_mfree) for every block of
  * >= 2 x 256 row groups: 0 = the library's measured table, 1 / 2 = cached
  * loads, 2 / 4 rows per group, 3 = non-temporal loads, 4 rows.  For tuning

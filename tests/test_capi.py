@@ -232,6 +232,3 @@ def test_every_cache_setter():
     assert [L.st_set_every_caps(c, caps[c]) for c in range(4)] == [3, 3, 3, 3]
     assert L.st_set_mfree_shape(4) < 0 and "st_set_mfree_shape" in _lib.last_error()
     assert L.st_set_mfree_shape(2) == 0 and L.st_set_mfree_shape(0) == 2
-    assert L.st_set_flat_fold(4) < 0 and "st_set_flat_fold" in _lib.last_error()
-    shipped_fold = L.st_set_flat_fold(0)
-    assert shipped_fold == 3 and L.st_set_flat_fold(shipped_fold) == 0

@@ -1355,51 +1355,3 @@ def test_deferred_writes_dropin_and_batches(eigen, orc):
     for batch in (1, 2, 5):
         got = eigen.similarity_transform_ex(mat, batch=batch)
         assert got[0] == ref[0] and np.array_equal(got[1], ref[1]) and got[3] == ref[3]
-
-
-@pytest.mark.parametrize("world,rank", [(16, 3), (14, 13)])
-def test_flat_fold_bitwise(world, rank):
-    """Folded long rows (st_set_flat_fold: a non-temporal block with rows of
-    >= 512 KiB walked as twice as many rows of half the length) move no
-    result: rank blocks of a 65536-column fp64 partition - 4096 rows at row
-    12288, and 4670 rows at row 60866, whose 9340 virtual rows leave the
-    deferred rounds' 8-row groups ragged - give bit-identical row sums, v,
-    state and block, every-round and deferred (a flush after a partial
-    group), folded or not."""
-    from eigen_value_amd import sharded
-    L = _lib.load()
-    n = 65536
-    saved = L.st_set_flat_fold(0)
-    try:
-        out = []
-        for mask in (0, 3):
-            assert L.st_set_flat_fold(mask) >= 0
-            sh = sharded.ShardedSimilarityTransform(n, torch.float64, rank_block=(world, rank))
-            p = sh.part
-            assert p.nrows * n * 8 >= (2 << 30) and sh.deferred_writes
-            sh.load("random", seed=5)
-            sh.start()
-            for _ in range(3):
-                sh.round(0.0, 1000)
-            every = (sh.s[sh.cur].clone(), sh.v.clone(), sh.mat.clone(),
-                     sh.ops.read_state(sh.state))
-            sh.load("random", seed=5)
-            sh.deferred_start()
-            for _ in range(9):
-                sh.deferred_round(0.0, 1000)
-            sh.deferred_flush(9, 0.0, 1000)
-            torch.cuda.synchronize()
-            defer = ([x.clone() for x in sh._ring[0]], sh.v.clone(), sh.mat.clone(),
-                     sh.ops.read_state(sh.state))
-            out.append((every, defer))
-            del sh
-            torch.cuda.empty_cache()
-        (e0, d0), (e1, d1) = out
-        for a, b in ((e0, e1), (d0, d1)):
-            s0, s1 = (a[0], b[0]) if isinstance(a[0], torch.Tensor) else (torch.stack(a[0]),
-                                                                          torch.stack(b[0]))
-            assert torch.equal(s0, s1)
-            assert torch.equal(a[1], b[1]) and torch.equal(a[2], b[2])
-            assert a[3] == b[3]
-    finally:
-        L.st_set_flat_fold(saved)

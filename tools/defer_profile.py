@@ -156,52 +156,6 @@ def run_every_ab(args):
     return out
 
 
-def run_fold_ab(args):
-    """--fold-ab 'm;m;...': folded long rows (st_set_flat_fold: bit 0 the
-    every-round launch, bit 1 the deferred rounds) - the every-round round
-    (--steps rounds) and the deferred store cycles (--cycles) under each
-    mask, interleaved over --passes repeats from a fresh A_0; prints and
-    returns the medians of both forms."""
-    import torch
-    import bench
-    from eigen_value_amd import _lib, sharded
-    L = _lib.load()
-    dt = torch.float64 if args.dtype == "f64" else torch.float32
-    rb = (args.rank_block, 0) if args.rank_block else None
-    sh = sharded.ShardedSimilarityTransform(args.n, dt, rank_block=rb)
-    sh.load(args.kind, seed=0)
-    specs = args.fold_ab.split(";")
-    res = {sp: {"every": [], "deferred": []} for sp in specs}
-    shipped = _lib.check(L.st_set_flat_fold(int(specs[0], 0)), "flat_fold")
-    bench.timed_rounds(sh, args.steps, 10, torch, None, 1)             # warm-up
-    bench.timed_deferred(sh, args.cycles, 2, torch, None, 1)
-    for _ in range(args.passes):
-        for sp in specs:
-            _lib.check(L.st_set_flat_fold(int(sp, 0)), "flat_fold")
-            sh.load(args.kind, seed=0)        # fresh A_0 per pass (see RELOAD_NOTE)
-            res[sp]["every"].append(bench.timed_rounds(sh, args.steps, 4, torch, None, 1)[1])
-            sh.load(args.kind, seed=0)
-            res[sp]["deferred"].append(
-                bench.timed_deferred(sh, args.cycles, 1, torch, None, 1)[1])
-    out = {"workload": f"{args.kind}{args.n}_{args.dtype}" + (
-               f" rank 0 of {args.rank_block}" if args.rank_block else ""),
-           "block": [sh.part.nrows, args.n],
-           "form": "every-round flat round and deferred store cycles, folded rows",
-           "steps": args.steps, "cycles": args.cycles, "passes": args.passes,
-           "ms_per_round": {}}
-    for sp in specs:
-        out["ms_per_round"][sp] = {}
-        for form in ("every", "deferred"):
-            v = sorted(res[sp][form])
-            out["ms_per_round"][sp][form] = {"median": v[len(v) // 2], "min": v[0],
-                                             "max": v[-1]}
-            print(f"{out['workload']} fold {sp:4s} {form:8s} median {v[len(v) // 2]:.5f} "
-                  f"ms/round (min {v[0]:.5f}, max {v[-1]:.5f})", flush=True)
-    L.st_set_flat_fold(shipped)
-    sh.close()
-    return out
-
-
 def set_defer_cache(mask, n, elem, nrows=None):
     """--defer-cache-ab: the deferred rounds' cache-policy flips for this
     block's dtype and size class (st_set_defer_cache: bit NP 0..4 = read-only
@@ -408,8 +362,6 @@ if __name__ == "__main__":
                    "(st_set_defer_cache, any dtype / size class) separated by ';'")
     p.add_argument("--mfree-ab", help="A/B of matrix-free launch shapes (st_set_mfree_shape: "
                    "0 table, 1 / 2 cached 2 / 4 rows, 3 non-temporal 4 rows) separated by ';'")
-    p.add_argument("--fold-ab", help="A/B of folded-row masks (st_set_flat_fold: bit 0 "
-                   "every-round, bit 1 deferred), both forms, separated by ';'")
     p.add_argument("--every-ab", help="A/B of every-round cache policies (st_set_every_cache: "
                    "0 the form's, 1 / 2 / 3 loads / stores / both turned over) separated by ';'")
     p.add_argument("--steps", type=int, default=100, help="with --every-ab: rounds per pass")
@@ -421,9 +373,8 @@ if __name__ == "__main__":
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
     wl = f"{a.kind}{a.n}_{a.dtype}"
-    if a.caps_ab or a.ntload_ab or a.every_ab or a.defer_cache_ab or a.mfree_ab or a.fold_ab:
-        r = (run_fold_ab(a) if a.fold_ab else
-             run_mfree_ab(a) if a.mfree_ab else
+    if a.caps_ab or a.ntload_ab or a.every_ab or a.defer_cache_ab or a.mfree_ab:
+        r = (run_mfree_ab(a) if a.mfree_ab else
              run_every_ab(a) if a.every_ab else run_caps_ab(a))
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)

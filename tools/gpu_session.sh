@@ -62,10 +62,6 @@ for s in $STEPS; do
       step bench_spawn_p2 900 python bench.py --gpus 2 --one-gpu --backend gloo --steps 20 --warmup 3 --no-overlap-leg ;;
     spawn8) # the driver's 8-GPU partition rehearsed: 8 self-spawned ranks on one GPU (gloo)
       step bench_spawn_p8 900 python bench.py --gpus 8 --one-gpu --backend gloo --steps 5 --warmup 1 ;;
-    fold) # folded long rows (st_set_flat_fold): bitwise tests, then the solve-loop A/B on configs[3]'s rank blocks
-      step pytest_fold 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread -k "flat_fold or every_cache_does_not or deferred_cache_flip or flat_2d_grid"
-      step foldab_p8 300 python -u tools/defer_profile.py --kind random --n 65536 --rank-block 8 --fold-ab "3;0" --passes 5 --steps 50 --cycles 4 --ab-json "$OUT/${RTAG}_foldab_random65536_p8_f64.json"
-      step foldab_p4 300 python -u tools/defer_profile.py --kind random --n 65536 --rank-block 4 --fold-ab "3;0" --passes 5 --steps 30 --cycles 3 --ab-json "$OUT/${RTAG}_foldab_random65536_p4_f64.json" ;;
     longrow) # configs[3]'s long-row rank blocks: column-block piece orders + the counter list
       rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
       FMS_EVERY=1 FMS_PT=4 FMS_PC=0,16,32,64 step longrow_pc 600 ./tools/flat_map_sweep f64 32768 8192x65536 16384x65536
