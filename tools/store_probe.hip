@@ -363,6 +363,10 @@ cap_sweep(const Block& b)
     one("store NP=5 R=8 PT=4 DS=1", [&](int k, unsigned l) { lib_launch<8, 5, NT, 1>(b, k, 4, true, l); }, true);
     one("store NP=5 R=8 PT=4", [&](int k, unsigned l) { lib_launch<8, 5, NT>(b, k, 4, true, l); }, true);
     one("store NP=5 R=4 PT=0", [&](int k, unsigned l) { lib_launch<4, 5, NT>(b, k, 0, true, l); }, true);
+    // two rows, the every-round launch's shape with the five pending scalings
+    one("store NP=5 R=2 PT=0 DS=1", [&](int k, unsigned l) { lib_launch<2, 5, NT, 1>(b, k, 0, true, l); }, true);
+    one("store NP=5 R=2 PT=4 DS=1", [&](int k, unsigned l) { lib_launch<2, 5, NT, 1>(b, k, 4, true, l); }, true);
+    one("store NP=5 R=2 PT=16 DS=1", [&](int k, unsigned l) { lib_launch<2, 5, NT, 1>(b, k, 16, true, l); }, true);
   } else {
     // cached fp64 blocks (< 2 GiB): 8 KB pieces
     one("every R=1 PT=8", [&](int k, unsigned l) { lib_launch<1, -1, NT>(b, k, 8, true, l); }, true);
