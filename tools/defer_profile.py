@@ -256,7 +256,16 @@ def summarise(path, n, elem, m, workload, events=None, launches=None):
     deferred launches themselves (kernel, NP, start, duration; one row per
     launch, in trace order) to this CSV - the trimmed trace that a committed
     summary cites, so its averages can be re-derived from tracked files."""
-    rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    rows = list(csv.DictReader(open(path)))
+    if rows and "Start_Timestamp" in rows[0]:
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    elif rows:
+        # a committed trimmed trace (--launches) re-summarised
+        rows = [{"Kernel_Name": r["kernel_name"], "Start_Timestamp": r["start_ns"],
+                 "End_Timestamp": str(int(r["start_ns"]) + int(r["duration_ns"]))}
+                for r in csv.DictReader(open(path))]
+        rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+        launches = None
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # noqa: E731
     flat, parts, last = {}, {}, None
     kept = []
@@ -281,14 +290,21 @@ def summarise(path, n, elem, m, workload, events=None, launches=None):
                             r["Kernel_Name"][:160]])
     nb = n * n * elem
     avg = lambda x: sum(x) / len(x)  # noqa: E731
+    # the steady state: the first store cycles of a trace run cold (the
+    # first storing launch 3.17 ms against 2.82 later at 32768^2 fp64), which
+    # the averages keep and the medians do not
+    med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
     out = {"workload": workload, "m": m,
            "trace": os.path.basename(launches) if launches else path,
            "k_flat": {}, "k_parts": {}}
     for pos in sorted(flat):
         t = avg(flat[pos])
         b = 2 * nb if pos in (-1, m - 1) else nb
+        tm = med(flat[pos])
         out["k_flat"][str(pos)] = {"launches": len(flat[pos]), "avg_ms": round(t, 5),
-                                   "bytes": b, "GBs": round(b / (t * 1e-3) / 1e9, 1)}
+                                   "median_ms": round(tm, 5),
+                                   "bytes": b, "GBs": round(b / (t * 1e-3) / 1e9, 1),
+                                   "GBs_median": round(b / (tm * 1e-3) / 1e9, 1)}
         if pos in parts:
             out["k_parts"][str(pos)] = round(avg(parts[pos]), 5)
         print(f"k_flat NP={pos}: {len(flat[pos])} launches, avg {t:.4f} ms "
@@ -299,6 +315,10 @@ def summarise(path, n, elem, m, workload, events=None, launches=None):
         out["cycle_ms_per_round"] = round(cyc, 5)
         by = (m + 1.0) / m * nb
         out["cycle_GBs"] = round(by / (cyc * 1e-3) / 1e9, 1)
+        cm = sum(med(flat[p]) + med(parts[p]) for p in range(m)) / m
+        out["cycle_ms_per_round_median"] = round(cm, 5)
+        out["cycle_GBs_median"] = round(by / (cm * 1e-3) / 1e9, 1)
+        print(f"steady state (medians): {cm:.4f} ms per round")
         print(f"one store cycle: {cyc:.4f} ms per round ({out['cycle_GBs']:.0f} GB/s on "
               f"(m+1)/m N^2 b)")
     if events:
