@@ -108,3 +108,12 @@ def test_defer_profile_cycle_and_launch_rows(tmp_path):
     assert len(launch_rows) == 2 * m * 2                      # k_flat + k_parts, no others
     assert {r["kernel"] for r in launch_rows} == {"k_flat", "k_parts"}
     assert launch_rows[0]["start_ns"] == "0" and launch_rows[0]["np"] == "0"
+    # the committed launches CSV re-summarises to the same figures, with the
+    # steady-state medians beside the averages
+    out2 = tmp_path / "cycle2.json"
+    subprocess.run([sys.executable, os.path.join(TOOLS, "defer_profile.py"), "--n", str(n),
+                    "--trace", str(lc), "--json", str(out2)], check=True, capture_output=True)
+    d2 = json.load(open(out2))
+    assert d2["cycle_ms_per_round"] == d["cycle_ms_per_round"]
+    assert d2["k_flat"]["5"]["median_ms"] == 0.002
+    assert d2["cycle_ms_per_round_median"] == d["cycle_ms_per_round_median"]
