@@ -101,6 +101,10 @@ def parse(argv=None):
                         "second stream) as the headline instead of an extra leg")
     p.add_argument("--no-overlap-leg", action="store_true",
                    help="N > 1: skip the extra overlapped-exchange leg")
+    p.add_argument("--stall-timeout", type=float, default=300.0,
+                   help="N > 1: seconds without progress after which a rank gives up "
+                        "(and the self-spawning parent ends the run) naming its last leg")
+    p.add_argument("--stall-rank", type=int, default=None, help=argparse.SUPPRESS)  # test hook
     p.add_argument("--leg", default=None, help=argparse.SUPPRESS)   # child mode
     p.add_argument("--leg-args", default="{}", help=argparse.SUPPRESS)
     p.add_argument("--one-gpu", action="store_true",
@@ -118,48 +122,136 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+HEARTBEAT_ENV = "ST_BENCH_HEARTBEAT"   # directory of per-rank progress files
+STALL_EXIT = 124                       # exit status of a run ended for no progress
+
+
+def _last_legs(hb_dir: str, n: int) -> dict:
+    """rank -> the last progress line it reported (heartbeat files)."""
+    out = {}
+    for r in range(n):
+        try:
+            with open(os.path.join(hb_dir, f"rank{r}")) as f:
+                out[r] = json.load(f)["leg"]
+        except (OSError, ValueError, KeyError):
+            out[r] = "(nothing reported)"
+    return out
+
+
+def spawn_ranks(n: int, argv, stall_timeout: float) -> int:
     """Start the N ranks of `bench.py argv` as child processes (this parent
     never initialises a GPU) and return the worst exit status.  A rank that
-    fails ends the others (by their own PIDs)."""
+    fails ends the others (by their own PIDs).  No-progress deadline: every
+    rank writes its progress lines to a heartbeat file; if no rank has
+    exited and none has reported for `stall_timeout` + 30 s (each rank's
+    own watchdog gives up after `stall_timeout`), the ranks are ended and
+    the parent exits with STALL_EXIT.  Either way, a failed run prints the
+    leg each rank last reported."""
+    import tempfile
     port = _free_port()
+    hb_dir = tempfile.mkdtemp(prefix="st_bench_hb_")
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                    LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env[HEARTBEAT_ENV] = hb_dir
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
                                       env=env))
     rcs = [None] * n
+    t_start = time.time()
+    stalled = False
+
+    def end_all():
+        for i, pr in enumerate(procs):
+            if rcs[i] is None:
+                pr.terminate()
+        for i, pr in enumerate(procs):
+            if rcs[i] is None:
+                try:
+                    rcs[i] = pr.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    pr.kill()
+                    rcs[i] = pr.wait()
+
     while any(rc is None for rc in rcs):
         for i, pr in enumerate(procs):
             if rcs[i] is None:
                 rcs[i] = pr.poll()
         if any(rc not in (None, 0) for rc in rcs):
-            for i, pr in enumerate(procs):
-                if rcs[i] is None:
-                    pr.terminate()
-            for i, pr in enumerate(procs):
-                if rcs[i] is None:
-                    try:
-                        rcs[i] = pr.wait(timeout=30)
-                    except subprocess.TimeoutExpired:
-                        pr.kill()
-                        rcs[i] = pr.wait()
+            end_all()
+            break
+        last = t_start
+        for r in range(n):
+            try:
+                last = max(last, os.path.getmtime(os.path.join(hb_dir, f"rank{r}")))
+            except OSError:
+                pass
+        if all(rc is None for rc in rcs) and time.time() - last > stall_timeout + 30:
+            stalled = True
+            end_all()
             break
         time.sleep(0.2)
     bad = [rc for rc in rcs if rc != 0]
+    if stalled or bad:
+        legs = _last_legs(hb_dir, n)
+        why = (f"no rank reported progress for {stall_timeout + 30:.0f} s" if stalled
+               else f"exit statuses {rcs}")
+        print(f"bench.py: {n}-rank run failed ({why}); last reported per rank:", file=sys.stderr)
+        for r in range(n):
+            print(f"bench.py:   rank {r} (exit {rcs[r]}): {legs[r]}", file=sys.stderr)
+        sys.stderr.flush()
+    import shutil
+    shutil.rmtree(hb_dir, ignore_errors=True)
+    if stalled:
+        return STALL_EXIT
     return (bad[0] if bad[0] > 0 else 1) if bad else 0
 
 
 _T0 = time.perf_counter()
 
 
+_BEAT = {"t": time.monotonic(), "leg": "start"}
+
+
 def progress(msg: str) -> None:
     """One line on stderr per finished leg (rank 0 only): long multi-rank
-    runs show they are alive, and a log shows where a failed run stopped."""
+    runs show they are alive, and a log shows where a failed run stopped.
+    Every rank also records it as its heartbeat (the watchdog below, and the
+    self-spawning parent's heartbeat file)."""
+    _BEAT["t"], _BEAT["leg"] = time.monotonic(), msg
+    hb = os.environ.get(HEARTBEAT_ENV)
+    if hb:
+        path = os.path.join(hb, f"rank{os.environ.get('RANK', '0')}")
+        try:
+            with open(path + ".tmp", "w") as f:
+                json.dump({"leg": msg, "t": time.time()}, f)
+            os.replace(path + ".tmp", path)
+        except OSError:
+            pass
     if os.environ.get("RANK", "0") == "0":
         print(f"[bench {time.perf_counter() - _T0:7.1f} s] {msg}", file=sys.stderr, flush=True)
+
+
+def start_watchdog(timeout: float) -> None:
+    """N > 1: a rank that reports no progress for `timeout` seconds (a peer
+    that never arrives at a collective, an RCCL or topology stall) prints
+    where it stopped and exits with STALL_EXIT, so the launcher
+    (torch.distributed.run, or spawn_ranks) ends the other ranks and the
+    run fails with the leg named instead of burning the step limit."""
+    import threading
+
+    def watch():
+        while True:
+            time.sleep(1.0)
+            idle = time.monotonic() - _BEAT["t"]
+            if idle > timeout:
+                print(f"bench.py: rank {os.environ.get('RANK', '0')}: no progress for "
+                      f"{idle:.0f} s after '{_BEAT['leg']}' (--stall-timeout {timeout:.0f}); "
+                      "giving up", file=sys.stderr, flush=True)
+                os._exit(STALL_EXIT)
+
+    threading.Thread(target=watch, name="bench-watchdog", daemon=True).start()
 
 
 def scaled_n(n1: int, world: int) -> int:
@@ -842,6 +934,19 @@ def strip_fracs(obj):
     return obj
 
 
+def stall_test(args, dist):
+    """--stall-rank R (tests/test_bench.py, CPU, gloo): rank R stops
+    reporting progress and never reaches the barrier the others wait in -
+    a stand-in for a rank stuck in RCCL init - so the watchdog and the
+    spawning parent's deadline can be tested without a GPU."""
+    dist.init_process_group("gloo")
+    progress("stall test: process group up")
+    if dist.get_rank() == args.stall_rank:
+        progress("stall test: this rank sleeps")
+        time.sleep(10 ** 6)
+    dist.barrier()
+
+
 # ---------------------------------------------------------------------------
 def main():
     args = parse()
@@ -849,11 +954,18 @@ def main():
         return leg_main(args)
     world_env = os.environ.get("WORLD_SIZE")
     if args.gpus > 1 and world_env is None:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.stall_timeout))
+    if args.gpus > 1 and os.environ.get("ST_BENCH_WATCHDOG", "1") != "0":
+        start_watchdog(args.stall_timeout)
+    progress("rank started")
 
     import numpy as np
     import torch
     import torch.distributed as dist
+
+    if args.stall_rank is not None:
+        return stall_test(args, dist)
+    progress("torch imported")
 
     from eigen_value_amd import sharded
     from eigen_value_amd import _lib
@@ -873,6 +985,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group("gloo")
+        progress(f"process group up ({args.backend}, world {world})")
     _lib.load()   # fail loudly before anything else if the HIP library is missing
     full = not args.no_north_star
 
@@ -882,6 +995,9 @@ def main():
     workload = f"{args.kind}{n}_{args.dtype}"
     sh = sharded.ShardedSimilarityTransform(n, dt, overlap=args.overlap)
     p = sh.part
+    if world > 1:
+        progress(f"{workload}: row blocks allocated, exchange "
+                 + ("library RCCL communicator" if sh.rccl is not None else "torch.distributed"))
 
     # ---- reference-semantics solve to convergence (EPS = 1e-3) ----------
     sh.load(args.kind)

@@ -198,6 +198,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_comm_init.restype = i32
     L.st_comm_destroy.argtypes = [P]
     L.st_comm_destroy.restype = i32
+    L.st_set_comm_timeout.argtypes = [ctypes.c_double]
+    L.st_set_comm_timeout.restype = ctypes.c_double
     L.st_comm_info.argtypes = [P, P, P, P]
     L.st_comm_info.restype = i32
     for sfx in ("f32", "f64"):

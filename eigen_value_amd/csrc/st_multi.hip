@@ -24,7 +24,9 @@
 #include <rccl/rccl.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "st_internal.h"
@@ -41,6 +43,95 @@ namespace {
       return -1;                                                               \
     }                                                                          \
   } while (0)
+
+// ---------------------------------------------------------------------------
+// deadline on every RCCL step that waits for peers.  Communicators are made
+// non-blocking (ncclConfig_t.blocking = 0), so ncclCommInitRankConfig and a
+// group's first collective (its connection setup) return ncclInProgress and
+// this thread polls ncclCommGetAsyncError until they finish or the deadline
+// passes; then the communicators are aborted and the call returns -1 with
+// the stalled rank and device named, instead of hanging in
+// ncclCommInitRank / ncclCommInitAll when a peer never arrives.
+// ---------------------------------------------------------------------------
+double g_comm_timeout_s = -1.0; // < 0: ST_COMM_TIMEOUT_S or 120 s
+
+double
+comm_timeout_s()
+{
+  if (g_comm_timeout_s >= 0.0)
+    return g_comm_timeout_s;
+  const char* e = std::getenv("ST_COMM_TIMEOUT_S");
+  const double v = e ? std::atof(e) : 0.0;
+  return v > 0.0 ? v : 120.0;
+}
+
+ncclConfig_t
+comm_config()
+{
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  return cfg;
+}
+
+// Wait until none of comms[0..n) is in progress.  ranks / devs name them
+// in the message.  Returns 0, or -1 (error set) on an asynchronous error or
+// when the deadline passes; on -1 the caller aborts the communicators.
+int
+comm_wait(const ncclComm_t* comms, int n, const int* ranks, const int* devs,
+          const char* what)
+{
+  const double limit = comm_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0;; spins++) {
+    int pending = -1;
+    for (int i = 0; i < n; i++) {
+      ncclResult_t st = ncclSuccess;
+      const ncclResult_t r = ncclCommGetAsyncError(comms[i], &st);
+      if (r != ncclSuccess)
+        st = r;
+      if (st == ncclInProgress) {
+        if (pending < 0)
+          pending = i;
+      } else if (st != ncclSuccess) {
+        ::st::set_error("%s: RCCL rank %d (device %d) failed: %s", what,
+                        ranks[i], devs[i], ncclGetErrorString(st));
+        return -1;
+      }
+    }
+    if (pending < 0)
+      return 0;
+    const double el = std::chrono::duration<double>(
+                        std::chrono::steady_clock::now() - t0)
+                        .count();
+    if (el > limit) {
+      ::st::set_error("%s: RCCL rank %d (device %d) still in progress after "
+                      "%.1f s (deadline %.1f s, ST_COMM_TIMEOUT_S / "
+                      "st_set_comm_timeout): a peer did not arrive; "
+                      "communicator aborted",
+                      what, ranks[pending], devs[pending], el, limit);
+      return -1;
+    }
+    if (spins > 64)
+      std::this_thread::sleep_for(std::chrono::microseconds(200));
+    else
+      std::this_thread::yield();
+  }
+}
+
+// the result of a call on non-blocking communicators: ncclInProgress is
+// waited for, anything else but ncclSuccess is an error
+int
+comm_settle(ncclResult_t r, const ncclComm_t* comms, int n, const int* ranks,
+            const int* devs, const char* what)
+{
+  if (r == ncclSuccess)
+    return 0;
+  if (r != ncclInProgress) {
+    ::st::set_error("%s failed: %s", what, ncclGetErrorString(r));
+    return -1;
+  }
+  return comm_wait(comms, n, ranks, devs, what);
+}
 
 template <typename T>
 ncclDataType_t
@@ -78,6 +169,9 @@ template <typename T>
 struct Multi
 {
   std::vector<Shard<T>> sh;
+  std::vector<ncclComm_t> comms; // sh[p].comm, for comm_wait
+  std::vector<int> ranks, devs;
+  bool abort = false; // a deadline passed: abort, do not destroy
   st_state* h_state = nullptr; // pinned, 2 slots
   hipEvent_t ev[2] = { nullptr, nullptr };
   ~Multi()
@@ -87,7 +181,7 @@ struct Multi
       if (d.stream)
         (void)hipStreamSynchronize(d.stream);
       if (d.comm)
-        (void)ncclCommDestroy(d.comm);
+        (void)(abort ? ncclCommAbort(d.comm) : ncclCommDestroy(d.comm));
       (void)hipFree(d.a);
       for (uint32_t i = 0; i <= kDeferRoundsMax; i++) {
         (void)hipFree(d.s[i]);
@@ -115,7 +209,9 @@ int
 gather(Multi<T>& M, int which, uint32_t chunk)
 {
   // P = 1 still issues the (in-place, no-op) collective, so the RCCL path
-  // is exercised on a one-GPU machine too
+  // is exercised on a one-GPU machine too.  On the non-blocking
+  // communicators the first group (connection setup) may return
+  // ncclInProgress: wait for it, under the deadline, before the next launch
   ST_NCCL(ncclGroupStart());
   for (size_t p = 0; p < M.sh.size(); p++) {
     Shard<T>& d = M.sh[p];
@@ -123,7 +219,11 @@ gather(Multi<T>& M, int which, uint32_t chunk)
     ST_NCCL(ncclAllGather(buf + p * chunk, buf, chunk, nccl_type<T>(), d.comm,
                           d.stream));
   }
-  ST_NCCL(ncclGroupEnd());
+  if (comm_settle(ncclGroupEnd(), M.comms.data(), (int)M.comms.size(),
+                  M.ranks.data(), M.devs.data(), "st_solve_multi all-gather")) {
+    M.abort = true;
+    return -1;
+  }
   return 0;
 }
 
@@ -227,10 +327,39 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   if (batch == 0) // as st_solve.hip: flat rounds are checked every 2 rounds
     batch = M.sh[0].part ? 2u : 8u;
   {
-    std::vector<ncclComm_t> comms(P);
-    ST_NCCL(ncclCommInitAll(comms.data(), (int)P, devlist.data()));
+    // ncclCommInitAll, but non-blocking and under the deadline: one id, a
+    // group of per-device ncclCommInitRankConfig calls, then poll
+    ncclUniqueId id;
+    ST_NCCL(ncclGetUniqueId(&id));
+    ncclConfig_t cfg = comm_config();
+    M.comms.assign(P, nullptr);
+    M.ranks.resize(P);
+    M.devs = devlist;
+    ST_NCCL(ncclGroupStart());
+    for (uint32_t p = 0; p < P; p++) {
+      M.ranks[p] = (int)p;
+      ST_CHECK(hipSetDevice(devlist[p]));
+      const ncclResult_t r =
+        ncclCommInitRankConfig(&M.comms[p], (int)P, id, (int)p, &cfg);
+      if (r != ncclSuccess && r != ncclInProgress) {
+        (void)ncclGroupEnd();
+        M.abort = true;
+        for (uint32_t q = 0; q <= p; q++)
+          M.sh[q].comm = M.comms[q];
+        ::st::set_error("st_solve_multi: ncclCommInitRankConfig (rank %u, "
+                        "device %d) failed: %s",
+                        p, devlist[p], ncclGetErrorString(r));
+        return -1;
+      }
+    }
+    const ncclResult_t ge = ncclGroupEnd();
     for (uint32_t p = 0; p < P; p++)
-      M.sh[p].comm = comms[p];
+      M.sh[p].comm = M.comms[p];
+    if (comm_settle(ge, M.comms.data(), (int)P, M.ranks.data(), M.devs.data(),
+                    "st_solve_multi communicator init")) {
+      M.abort = true;
+      return -1;
+    }
   }
   for (uint32_t p = 0; p < P; p++) { // s_0 = rowsum(A_0), then gather
     Shard<T>& d = M.sh[p];
@@ -355,6 +484,30 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
 } // namespace
 } // namespace st
 
+// ---------------------------------------------------------------------------
+// one-process-per-GPU communicator (the sharded driver's RCCL path): rank 0
+// makes the 128-byte unique id, the caller broadcasts it (torch.distributed
+// over TCP), every rank joins; the all-gather is then issued directly on
+// the launch stream, with no cross-stream hand-off per round.  The handle
+// is a CommBox: the non-blocking communicator plus the rank and device its
+// deadline messages name.
+// ---------------------------------------------------------------------------
+namespace st {
+namespace {
+struct CommBox
+{
+  ncclComm_t c = nullptr;
+  int rank = 0, dev = 0;
+};
+
+int
+comm_collective(CommBox* b, ncclResult_t r, const char* what)
+{
+  return comm_settle(r, &b->c, 1, &b->rank, &b->dev, what);
+}
+} // namespace
+} // namespace st
+
 extern "C" {
 
 int64_t
@@ -382,12 +535,15 @@ st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
                                  eigen_val, eigen_vec, iter_cnt, opt, stats);
 }
 
-// ---------------------------------------------------------------------------
-// one-process-per-GPU communicator (the sharded driver's RCCL path): rank 0
-// makes the 128-byte unique id, the caller broadcasts it (torch.distributed
-// over TCP), every rank joins; the all-gather is then issued directly on
-// the launch stream, with no cross-stream hand-off per round.
-// ---------------------------------------------------------------------------
+
+double
+st_set_comm_timeout(double seconds)
+{
+  const double old = st::comm_timeout_s();
+  st::g_comm_timeout_s = seconds > 0.0 ? seconds : -1.0;
+  return old;
+}
+
 int
 st_comm_unique_id(char* id_out /* NCCL_UNIQUE_ID_BYTES */)
 {
@@ -410,9 +566,18 @@ st_comm_init(void** comm, int nranks, int rank, const char* id_in, int device)
   ST_CHECK(hipSetDevice(device));
   ncclUniqueId id;
   std::memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);
-  ncclComm_t c = nullptr;
-  ST_NCCL(ncclCommInitRank(&c, nranks, id, rank));
-  *comm = c;
+  auto* b = new st::CommBox;
+  b->rank = rank;
+  b->dev = device;
+  ncclConfig_t cfg = st::comm_config();
+  const ncclResult_t r = ncclCommInitRankConfig(&b->c, nranks, id, rank, &cfg);
+  if (st::comm_collective(b, r, "st_comm_init")) {
+    if (b->c)
+      (void)ncclCommAbort(b->c);
+    delete b;
+    return -1;
+  }
+  *comm = b;
   return 0;
 }
 
@@ -421,8 +586,17 @@ st_comm_destroy(void* comm)
 {
   st::clear_error();
   st::DeviceGuard guard;
-  if (comm)
-    ST_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+  if (!comm)
+    return 0;
+  auto* b = static_cast<st::CommBox*>(comm);
+  // finalize (flushes this rank's collectives; non-blocking, so under the
+  // deadline), then free; a communicator that cannot finalize is aborted
+  int rc = st::comm_collective(b, ncclCommFinalize(b->c), "st_comm_destroy");
+  const ncclResult_t r = rc ? ncclCommAbort(b->c) : ncclCommDestroy(b->c);
+  delete b;
+  if (rc)
+    return -1;
+  ST_NCCL(r);
   return 0;
 }
 
@@ -431,7 +605,7 @@ st_comm_info(void* comm, int* nranks, int* rank, int* device)
 {
   st::clear_error();
   ST_REQUIRE(comm, "st_comm_info: null communicator");
-  const ncclComm_t c = reinterpret_cast<ncclComm_t>(comm);
+  const ncclComm_t c = static_cast<st::CommBox*>(comm)->c;
   if (nranks)
     ST_NCCL(ncclCommCount(c, nranks));
   if (rank)
@@ -447,10 +621,12 @@ st_allgather_f32(void* comm, const float* send, float* recv, uint64_t count,
 {
   st::clear_error();
   ST_REQUIRE(comm && send && recv, "st_allgather: null pointer");
-  ST_NCCL(ncclAllGather(send, recv, count, ncclFloat,
-                        reinterpret_cast<ncclComm_t>(comm),
-                        reinterpret_cast<hipStream_t>(stream)));
-  return 0;
+  auto* b = static_cast<st::CommBox*>(comm);
+  return st::comm_collective(
+    b,
+    ncclAllGather(send, recv, count, ncclFloat, b->c,
+                  reinterpret_cast<hipStream_t>(stream)),
+    "st_allgather");
 }
 
 int
@@ -459,10 +635,12 @@ st_allgather_f64(void* comm, const double* send, double* recv, uint64_t count,
 {
   st::clear_error();
   ST_REQUIRE(comm && send && recv, "st_allgather: null pointer");
-  ST_NCCL(ncclAllGather(send, recv, count, ncclDouble,
-                        reinterpret_cast<ncclComm_t>(comm),
-                        reinterpret_cast<hipStream_t>(stream)));
-  return 0;
+  auto* b = static_cast<st::CommBox*>(comm);
+  return st::comm_collective(
+    b,
+    ncclAllGather(send, recv, count, ncclDouble, b->c,
+                  reinterpret_cast<hipStream_t>(stream)),
+    "st_allgather");
 }
 
 } // extern "C"

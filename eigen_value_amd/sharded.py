@@ -184,16 +184,17 @@ class RcclComm:
         rank = dist.get_rank(group)
         dev = torch.cuda.current_device() if device_index is None else device_index
         uid = ctypes.create_string_buffer(128)
-        # rank 0's failure to make an id reaches every rank (None is
-        # broadcast), so no rank is left waiting in ncclCommInitRank
+        # rank 0's failure to make an id reaches every rank (its error text
+        # is broadcast instead of the id), so no rank enters st_comm_init
         obj = [None]
-        if rank == 0 and self.L.st_comm_unique_id(uid) == 0:
-            obj = [uid.raw]
+        if rank == 0:
+            obj = ([uid.raw] if self.L.st_comm_unique_id(uid) == 0
+                   else [("error", _lib.last_error())])
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
                                    group=group)
         self.comm = ctypes.c_void_p()
-        if obj[0] is None:
-            raise _lib.EigenValueError("st_comm_unique_id failed on rank 0")
+        if isinstance(obj[0], tuple):
+            raise _lib.EigenValueError(f"st_comm_unique_id failed on rank 0: {obj[0][1]}")
         _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, obj[0], dev),
                    "st_comm_init")
         self.rank, self.world = rank, world
@@ -223,7 +224,11 @@ def make_comm_agreed(group, factory, device=None):
     whether it succeeded: a communicator is used only if EVERY rank has one
     - otherwise all ranks close theirs and return (None, reason), so no rank
     issues the library all-gather while another waits in torch's (a mixed
-    exchange would hang the first round)."""
+    exchange would hang the first round).  Every rank reaches the
+    all-reduce: rank 0's id failure is broadcast before anyone joins, and a
+    rank whose st_comm_init fails leaves its peers waiting only until the
+    library's RCCL deadline (st_set_comm_timeout, ST_COMM_TIMEOUT_S), after
+    which their st_comm_init aborts and returns an error too."""
     import torch
     import torch.distributed as dist
     comm, err = None, None

@@ -184,11 +184,23 @@ int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
 /* One-process-per-GPU RCCL communicator for the sharded step API: rank 0
  * calls st_comm_unique_id (128 bytes), the caller distributes the id, every
  * rank calls st_comm_init (nranks, its rank, its HIP device).  st_allgather
- * is ncclAllGather on `stream` (in place when send = recv + rank*count). */
+ * is ncclAllGather on `stream` (in place when send = recv + rank*count).
+ *
+ * Deadline: every communicator is non-blocking (ncclConfig_t.blocking = 0)
+ * and each step that waits for peers - st_comm_init, a collective's
+ * connection setup, st_comm_destroy, and the communicator setup and
+ * all-gathers of st_solve_multi_* - is polled (ncclCommGetAsyncError) for at
+ * most st_set_comm_timeout() seconds (default: the environment variable
+ * ST_COMM_TIMEOUT_S, else 120).  Past it the communicator is aborted
+ * (ncclCommAbort) and the call returns -1; eigen_last_error() names the
+ * RCCL rank and HIP device still in progress. */
 int st_comm_unique_id(char* id_out);
 int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
                  int device);
 int st_comm_destroy(void* comm);
+/* Set the RCCL deadline in seconds (<= 0: back to ST_COMM_TIMEOUT_S / 120);
+ * returns the previous effective value.  Process-wide. */
+double st_set_comm_timeout(double seconds);
 /* What the communicator itself reports (ncclCommCount / ncclCommUserRank /
  * ncclCommCuDevice): the ranks RCCL joined, this rank, its HIP device.
  * Any output pointer may be NULL.  Returns 0 or negative. */

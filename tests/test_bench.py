@@ -85,6 +85,45 @@ def test_self_spawned_ranks_report_failure():
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
 
 
+def _stalled_run(watchdog: bool, stall_timeout: float, limit: float):
+    """`bench.py --gpus 2 --backend gloo` with rank 1 asleep after the process
+    group comes up (the --stall-rank hook: a stand-in for a rank stuck in
+    RCCL init) while rank 0 waits for it in a barrier."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["ST_BENCH_WATCHDOG"] = "1" if watchdog else "0"
+    import time
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2",
+                          "--backend", "gloo", "--stall-rank", "1",
+                          "--stall-timeout", str(stall_timeout)],
+                         capture_output=True, text=True, timeout=limit, cwd=REPO, env=env)
+    return out, time.time() - t0
+
+
+def test_stalled_rank_is_named_by_its_watchdog():
+    """A rank that never progresses ends the run within the deadline: the
+    ranks' own watchdogs give up after --stall-timeout, the parent ends the
+    other rank and prints where each one stopped, and exits non-zero with
+    no JSON line (VERDICT r03 'next' #1)."""
+    out, el = _stalled_run(True, 4, 240)
+    assert out.returncode != 0, out.stderr[-3000:]
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert "no progress for" in out.stderr
+    assert "rank 1 (exit" in out.stderr and "stall test: this rank sleeps" in out.stderr
+    assert "rank 0 (exit" in out.stderr and "stall test: process group up" in out.stderr
+
+
+def test_stalled_ranks_are_ended_by_the_parent_deadline():
+    """With the ranks' watchdogs off (a rank wedged where its watchdog thread
+    cannot run), the self-spawning parent's own no-progress deadline
+    (--stall-timeout + 30 s) ends both ranks and exits with STALL_EXIT."""
+    out, el = _stalled_run(False, 2, 240)
+    assert out.returncode == bench.STALL_EXIT, out.stderr[-3000:]
+    assert "no rank reported progress" in out.stderr
+    assert "rank 1 (exit" in out.stderr and "stall test: this rank sleeps" in out.stderr
+    assert el < 200
+
+
 @pytest.mark.gpu
 def test_bench_self_spawned_two_ranks_on_one_gpu():
     """The N > 1 line without torch.distributed.run: two self-spawned ranks

@@ -232,3 +232,29 @@ def test_every_cache_setter():
     assert [L.st_set_every_caps(c, caps[c]) for c in range(4)] == [3, 3, 3, 3]
     assert L.st_set_mfree_shape(4) < 0 and "st_set_mfree_shape" in _lib.last_error()
     assert L.st_set_mfree_shape(2) == 0 and L.st_set_mfree_shape(0) == 2
+
+
+def test_comm_timeout_setter_and_env(monkeypatch):
+    """st_set_comm_timeout: the RCCL deadline every waiting communicator step
+    is polled under (default ST_COMM_TIMEOUT_S, else 120 s); a value <= 0
+    restores the default.  No GPU needed: the setter is host state."""
+    L = _lib.load()
+    base = L.st_set_comm_timeout(0.0)                   # reset, read the default
+    assert base == float(os.environ.get("ST_COMM_TIMEOUT_S", "120") or 120)
+    assert L.st_set_comm_timeout(7.5) == base
+    assert L.st_set_comm_timeout(-1.0) == 7.5
+    assert L.st_set_comm_timeout(0.0) == base
+
+
+def test_comm_calls_reject_bad_arguments_without_a_device():
+    """st_comm_init validates before touching RCCL or HIP, and a NULL
+    communicator is an error everywhere but st_comm_destroy (a no-op)."""
+    L = _lib.load()
+    comm = ctypes.c_void_p(123)
+    assert L.st_comm_init(ctypes.byref(comm), 2, 2, b"\0" * 128, 0) < 0
+    assert "bad rank" in _lib.last_error()
+    assert L.st_comm_init(None, 1, 0, b"\0" * 128, 0) < 0
+    assert L.st_comm_info(None, None, None, None) < 0
+    assert L.st_comm_destroy(None) == 0
+    buf = (ctypes.c_double * 4)()
+    assert L.st_allgather_f64(None, buf, buf, 1, None) < 0
