@@ -26,6 +26,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <memory>
 #include <thread>
 #include <vector>
 
@@ -116,6 +118,75 @@ comm_wait(const ncclComm_t* comms, int n, const int* ranks, const int* devs,
     else
       std::this_thread::yield();
   }
+}
+
+// Communicator creation under the deadline.  RCCL 2.27's
+// ncclCommInitRankConfig does not return to its caller while a peer is
+// missing, non-blocking config or not (tools/comm_deadline_probe.cpp,
+// profiles/r04_comm_deadline_probe.log), so the init runs on a helper
+// thread and this thread waits for it at most the deadline.  Past it the
+// call fails with the stalled rank named; any handle RCCL already wrote is
+// aborted from another detached thread (ncclCommAbort may itself wait for
+// the init), and the helper is left behind - the caller is expected to end
+// the job, which is what the deadline is for.
+struct InitJob
+{
+  std::vector<ncclComm_t> comms; // written by RCCL (early, non-blocking config)
+  ncclResult_t r = ncclInProgress;
+  int done = 0; // __atomic
+};
+
+int
+init_with_deadline(const std::shared_ptr<InitJob>& job,
+                   std::function<ncclResult_t(InitJob&)> body, const int* ranks,
+                   const int* devs, const char* what)
+{
+  std::thread([job, body]() {
+    const ncclResult_t r = body(*job);
+    job->r = r;
+    __atomic_store_n(&job->done, 1, __ATOMIC_RELEASE);
+  }).detach();
+  const double limit = comm_timeout_s();
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    if (__atomic_load_n(&job->done, __ATOMIC_ACQUIRE))
+      break;
+    const double el = std::chrono::duration<double>(
+                        std::chrono::steady_clock::now() - t0)
+                        .count();
+    if (el > limit) {
+      const int n = (int)job->comms.size();
+      for (int i = 0; i < n; i++) {
+        ncclComm_t c = __atomic_load_n(&job->comms[i], __ATOMIC_ACQUIRE);
+        if (c)
+          std::thread([c]() { (void)ncclCommAbort(c); }).detach();
+      }
+      ::st::set_error("%s: RCCL rank %d (device %d) still in progress after "
+                      "%.1f s (deadline %.1f s, ST_COMM_TIMEOUT_S / "
+                      "st_set_comm_timeout): ncclCommInitRankConfig did not "
+                      "return - a peer did not arrive; communicator aborted",
+                      what, ranks[0], devs[0], el, limit);
+      return -1;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(500));
+  }
+  // returned: it may still be finishing asynchronously (ncclInProgress)
+  if (job->r != ncclSuccess && job->r != ncclInProgress) {
+    ::st::set_error("%s: ncclCommInitRankConfig (RCCL rank %d, device %d) "
+                    "failed: %s",
+                    what, ranks[0], devs[0], ncclGetErrorString(job->r));
+    for (ncclComm_t c : job->comms)
+      if (c)
+        (void)ncclCommAbort(c);
+    return -1;
+  }
+  if (comm_wait(job->comms.data(), (int)job->comms.size(), ranks, devs, what)) {
+    for (ncclComm_t c : job->comms)
+      if (c)
+        (void)ncclCommAbort(c);
+    return -1;
+  }
+  return 0;
 }
 
 // the result of a call on non-blocking communicators: ncclInProgress is
@@ -327,38 +398,43 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   if (batch == 0) // as st_solve.hip: flat rounds are checked every 2 rounds
     batch = M.sh[0].part ? 2u : 8u;
   {
-    // ncclCommInitAll, but non-blocking and under the deadline: one id, a
-    // group of per-device ncclCommInitRankConfig calls, then poll
+    // ncclCommInitAll, but under the deadline: one id, a group of
+    // per-device non-blocking ncclCommInitRankConfig calls on a helper
+    // thread (init_with_deadline), then poll
     ncclUniqueId id;
     ST_NCCL(ncclGetUniqueId(&id));
-    ncclConfig_t cfg = comm_config();
-    M.comms.assign(P, nullptr);
     M.ranks.resize(P);
-    M.devs = devlist;
-    ST_NCCL(ncclGroupStart());
-    for (uint32_t p = 0; p < P; p++) {
-      M.ranks[p] = (int)p;
-      ST_CHECK(hipSetDevice(devlist[p]));
-      const ncclResult_t r =
-        ncclCommInitRankConfig(&M.comms[p], (int)P, id, (int)p, &cfg);
-      if (r != ncclSuccess && r != ncclInProgress) {
-        (void)ncclGroupEnd();
-        M.abort = true;
-        for (uint32_t q = 0; q <= p; q++)
-          M.sh[q].comm = M.comms[q];
-        ::st::set_error("st_solve_multi: ncclCommInitRankConfig (rank %u, "
-                        "device %d) failed: %s",
-                        p, devlist[p], ncclGetErrorString(r));
-        return -1;
-      }
-    }
-    const ncclResult_t ge = ncclGroupEnd();
     for (uint32_t p = 0; p < P; p++)
-      M.sh[p].comm = M.comms[p];
-    if (comm_settle(ge, M.comms.data(), (int)P, M.ranks.data(), M.devs.data(),
-                    "st_solve_multi communicator init")) {
-      M.abort = true;
-      return -1;
+      M.ranks[p] = (int)p;
+    M.devs = devlist;
+    auto job = std::make_shared<InitJob>();
+    job->comms.assign(P, nullptr);
+    const std::vector<int> devs = devlist;
+    const int rc = init_with_deadline(
+      job,
+      [id, devs](InitJob& j) {
+        ncclConfig_t cfg = comm_config();
+        ncclResult_t r = ncclGroupStart();
+        for (size_t p = 0; p < devs.size() && (r == ncclSuccess); p++) {
+          if (hipSetDevice(devs[p]) != hipSuccess)
+            r = ncclUnhandledCudaError;
+          else {
+            const ncclResult_t q = ncclCommInitRankConfig(
+              &j.comms[p], (int)devs.size(), id, (int)p, &cfg);
+            if (q != ncclSuccess && q != ncclInProgress)
+              r = q;
+          }
+        }
+        const ncclResult_t ge = ncclGroupEnd();
+        return r != ncclSuccess ? r : ge;
+      },
+      M.ranks.data(), M.devs.data(), "st_solve_multi communicator init");
+    if (rc == 0) {
+      M.comms = job->comms;
+      for (uint32_t p = 0; p < P; p++)
+        M.sh[p].comm = M.comms[p];
+    } else {
+      return -1; // the communicators were aborted (or are left to the helper)
     }
   }
   for (uint32_t p = 0; p < P; p++) { // s_0 = rowsum(A_0), then gather
@@ -566,17 +642,22 @@ st_comm_init(void** comm, int nranks, int rank, const char* id_in, int device)
   ST_CHECK(hipSetDevice(device));
   ncclUniqueId id;
   std::memcpy(id.internal, id_in, NCCL_UNIQUE_ID_BYTES);
+  auto job = std::make_shared<st::InitJob>();
+  job->comms.assign(1, nullptr);
+  if (st::init_with_deadline(
+        job,
+        [id, nranks, rank, device](st::InitJob& j) {
+          if (hipSetDevice(device) != hipSuccess)
+            return ncclUnhandledCudaError;
+          ncclConfig_t cfg = st::comm_config();
+          return ncclCommInitRankConfig(&j.comms[0], nranks, id, rank, &cfg);
+        },
+        &rank, &device, "st_comm_init"))
+    return -1;
   auto* b = new st::CommBox;
+  b->c = job->comms[0];
   b->rank = rank;
   b->dev = device;
-  ncclConfig_t cfg = st::comm_config();
-  const ncclResult_t r = ncclCommInitRankConfig(&b->c, nranks, id, rank, &cfg);
-  if (st::comm_collective(b, r, "st_comm_init")) {
-    if (b->c)
-      (void)ncclCommAbort(b->c);
-    delete b;
-    return -1;
-  }
   *comm = b;
   return 0;
 }

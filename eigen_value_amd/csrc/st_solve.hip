@@ -454,7 +454,7 @@ st_version(void)
   // the A/B probe switches the kernels were built with (st_kernels.hip):
   // "defaults" in every library build, the values in a probe build
   static const std::string v =
-    std::string("eigen_value_amd 0.3.0 (gfx950; probe switches: ") +
+    std::string("eigen_value_amd 0.4.0 (gfx950; probe switches: ") +
     st_probe_switches() + ")";
   return v.c_str();
 }

@@ -258,3 +258,10 @@ def test_comm_calls_reject_bad_arguments_without_a_device():
     assert L.st_comm_destroy(None) == 0
     buf = (ctypes.c_double * 4)()
     assert L.st_allgather_f64(None, buf, buf, 1, None) < 0
+
+
+def test_package_and_library_versions_agree():
+    """eigen_value_amd.__version__ is the version st_version() reports."""
+    import eigen_value_amd
+    L = _lib.load()
+    assert L.st_version().decode().split()[1] == eigen_value_amd.__version__

@@ -117,3 +117,18 @@ def test_defer_profile_cycle_and_launch_rows(tmp_path):
     assert d2["cycle_ms_per_round"] == d["cycle_ms_per_round"]
     assert d2["k_flat"]["5"]["median_ms"] == 0.002
     assert d2["cycle_ms_per_round_median"] == d["cycle_ms_per_round_median"]
+
+
+def test_citation_checker_expands_ellipsis_names():
+    """tools/check_citations.py reads `name.log, …_X_table.txt` as the full
+    name the ellipsis abbreviates (its --rm pass had deleted two
+    tables cited that way), and every tracked profile is cited."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import check_citations as cc
+    assert cc.expand_ellipsis("r01_sweep_dir_blocks.log", "_blocks_table.txt") == \
+        "r01_sweep_dir_blocks_table.txt"
+    assert cc.expand_ellipsis("r03_defer_cycle_x.json", "_launches.csv") == \
+        "r03_defer_cycle_x_launches.csv"
+    pats = cc.cited_patterns()
+    assert "r01_sweep_dir_policy_table.txt" in pats
+    assert cc.uncited() == []

@@ -32,13 +32,37 @@ def braces(p):
         braces(p[:m.start()] + alt + p[m.end():]) for alt in m.group(1).split(",")))
 
 
+ELLIPSIS = re.compile(r"…(_[A-Za-z0-9_*{},.\-\[\]]+)")
+
+
+def expand_ellipsis(prev, tail):
+    """`…_X` after a full name on the same line: the shared prefix of `prev`
+    up to where X's first word starts in it (`r01_sweep_dir_blocks.log`,
+    `…_blocks_table.txt` -> `r01_sweep_dir_blocks_table.txt`), else prev
+    without its extension + tail (`r03_defer_cycle_x.json` + `…_launches.csv`)."""
+    tail = tail.rstrip(".,")
+    word = re.match(r"_[A-Za-z0-9]+", tail).group(0)
+    i = prev.rfind(word)
+    if i > 0:
+        return prev[:i] + tail
+    return os.path.splitext(prev)[0] + tail
+
+
 def cited_patterns():
     pats = set()
     for pat in SOURCES:
         for f in glob.glob(os.path.join(HERE, pat)):
-            if os.path.isfile(f):
-                for tok in TOKEN.findall(open(f, errors="replace").read()):
-                    tok = tok.rstrip(".,")
+            if not os.path.isfile(f):
+                continue
+            for line in open(f, errors="replace").read().splitlines():
+                prev = None
+                for m in re.finditer(TOKEN.pattern + "|" + ELLIPSIS.pattern, line):
+                    if m.group(0).startswith("…"):
+                        if prev is None:
+                            continue
+                        tok = expand_ellipsis(prev, m.group(1))
+                    else:
+                        tok = prev = m.group(0).rstrip(".,")
                     for p in braces(tok):
                         pats.add(p)
     return pats

@@ -24,14 +24,15 @@ dt = torch.float32 if a.f32 else torch.float64
 n, D = a.n, "cuda:0"
 mat = dev.generate("random", n, dt, seed=0, device=D)
 g = torch.Generator(device="cpu").manual_seed(1)
+m = dev.defer_rounds(n, n, dt)
+# s_k plus m - 1 pending vectors (the storing round re-applies m - 1)
 vecs = [(torch.rand(n, generator=g, dtype=torch.float64) * n / 2 + n / 4).to(dt).to(D)
-        for _ in range(4)]
+        for _ in range(m)]
 invs = [1.0 / x for x in vecs]
 s_next, inv_next = torch.empty(n, dtype=dt, device=D), torch.empty(n, dtype=dt, device=D)
 v = torch.ones(n, dtype=dt, device=D)
 part = dev.flat_scratch(n, n, dt, D)
 state = dev.new_state(D)
-m = dev.defer_rounds(n, n, dt)
 print(f"n={n} {dt} rounds per store {m}", flush=True)
 
 
@@ -52,7 +53,9 @@ def run(npend, alias, store=False, k0=1):
     return min(times), sorted(times)[len(times) // 2]
 
 
-for npend in range(m):
+# read-only rounds carry 0 .. m - 2 pending scalings (m - 1 pending is the
+# storing round, which a non-storing call is refused)
+for npend in range(m - 1):
     for alias in (False, True):
         if npend == 0 and alias:
             continue

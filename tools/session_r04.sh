@@ -1,0 +1,39 @@
+# round-4 GPU session steps (one file, rewritten per session; earlier
+# sessions' steps are in tools/gpu_session.sh)
+set -u
+O=gpurun_out/${S:-r04_s3}; mkdir -p $O
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+fail() { echo "== stopping: $1 exited $2"; exit $2; }
+run() { # name secs cmd...  (rc 0/1 continue; anything else ends the session)
+  local n=$1 t=$2; shift 2
+  echo "== $n: $*"; local t0=$(date +%s)
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "== $n rc=$rc ($(( $(date +%s) - t0 ))s)"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then fail $n $rc; fi
+}
+for step in ${STEPS:-cdp stagger deferweak l2 tests}; do case $step in
+cdp)
+  # not run under run(): a hang here is the finding, and it ends only this probe
+  CDP_THREAD=1 CDP_ABORT=0 timeout -k 5 30 ./tools/comm_deadline_probe > $O/cdp_thread_noabort.log 2>&1; echo "cdp_thread_noabort rc=$?"
+  CDP_THREAD=1 CDP_ABORT=1 timeout -k 5 30 ./tools/comm_deadline_probe > $O/cdp_thread_abort.log 2>&1; echo "cdp_thread_abort rc=$?" ;;
+stagger) run stagger 400 ./tools/stagger_probe 32768x32768 8192x65536 ;;
+deferweak)
+  for W in "8192 0" "11648 2" "16384 4" "23040 8"; do
+    set -- $W; N=$1; P=$2; D=$O/defer_h${N}_p${P}; mkdir -p $D
+    run defer_h${N}_p${P} 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --cycles 10 --events $D/events.json
+    python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --trace $D/prof/run_kernel_trace.csv --events $D/events.json --json $O/r04_defer_cycle_hilbert${N}_p${P}_f64.json --launches $O/r04_defer_cycle_hilbert${N}_p${P}_f64_launches.csv > $D/summary.txt 2>&1
+    cat $D/summary.txt
+  done ;;
+l2)
+  for W in "32768 0" "65536 8"; do
+    set -- $W; N=$1; P=$2; D=$O/l2_r${N}_p${P}; mkdir -p $D
+    run l2_tcc_defer_${N} 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d $D/tcc_defer -o run -- python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype f64 --cycles 2
+    run l2_tcp_defer_${N} 180 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_ACCESSES_sum --output-format csv -d $D/tcp_defer -o run -- python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype f64 --cycles 2
+    run l2_tcc_every_${N} 180 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum TCC_REQ_sum --output-format csv -d $D/tcc_every -o run -- python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype f64 --every-ab 0 --steps 8 --passes 1
+    run l2_tcp_every_${N} 180 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_ACCESSES_sum --output-format csv -d $D/tcp_every -o run -- python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype f64 --every-ab 0 --steps 8 --passes 1
+    python3 tools/sq_counters.py $D/tcc_defer/run_counter_collection.csv $D/tcp_defer/run_counter_collection.csv $D/tcc_every/run_counter_collection.csv $D/tcp_every/run_counter_collection.csv --json=$O/r04_l2_random${N}_p${P}_f64.json
+  done ;;
+tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
+bench) run bench 600 python bench.py ;;
+esac; done
+echo "== session done"
