@@ -35,6 +35,9 @@
 #ifndef ST_DEFER_STORE_R8_CACHED // 8 rows for the cached fp64 5-pending store
 #define ST_DEFER_STORE_R8_CACHED 1
 #endif
+#ifndef ST_DEFER_TS5_CACHED // its piece tile (row groups; 0 = row-major)
+#define ST_DEFER_TS5_CACHED 4u
+#endif
 #ifndef ST_FLAT_ALT // the flat launches' odd-round order (2 = reversed per XCD, 0 = none)
 #define ST_FLAT_ALT 2
 #endif
@@ -42,7 +45,7 @@
   (ST_DPP_NOINIT == 1 && ST_ROW_VLOAD == 0 && ST_FLAT_UNMASKED == 1 &&         \
    ST_DEFER_STORE_NT == 0 && ST_EVERY_CACHED_R1 == 1 &&                        \
    ST_DEFER_R0_CACHED == 1 && ST_DEFER_PT0_CACHED == 4 &&                      \
-   ST_DEFER_STORE_R8_CACHED == 1 && ST_FLAT_ALT == 2)
+   ST_DEFER_STORE_R8_CACHED == 1 && ST_DEFER_TS5_CACHED == 4 && ST_FLAT_ALT == 2)
 #ifndef ST_PROBES
 static_assert(ST_PROBES_DEFAULT,
               "A/B probe switch set in a library build (use -DST_PROBES=1)");
@@ -1062,7 +1065,7 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr bool kS8 = !NT && sizeof(T) == 8 && ST_DEFER_STORE_R8_CACHED;
   constexpr int kRS = NT ? 8 : 4;
   constexpr int kRS5 = kS8 ? 8 : kRS;
-  constexpr uint32_t kTileS5 = kS8 ? 4u : 0u;
+  constexpr uint32_t kTileS5 = kS8 ? ST_DEFER_TS5_CACHED : 0u;
   constexpr int kR2 = NT ? 8 : 4; // NP = 2: 1-2 % with 8 rows, non-temporal only
   static_assert(kDeferRoundsMax == 6, "one case per pending count below");
   if (store) {
@@ -1712,7 +1715,8 @@ st_probe_switches(void)
                    " ST_DEFER_R0_CACHED=" ST_STR(ST_DEFER_R0_CACHED)
                      " ST_DEFER_PT0_CACHED=" ST_STR(ST_DEFER_PT0_CACHED)
                        " ST_DEFER_STORE_R8_CACHED=" ST_STR(
-                         ST_DEFER_STORE_R8_CACHED) " ST_FLAT_ALT=" ST_STR(ST_FLAT_ALT);
+                         ST_DEFER_STORE_R8_CACHED) " ST_DEFER_TS5_CACHED=" ST_STR(
+                           ST_DEFER_TS5_CACHED) " ST_FLAT_ALT=" ST_STR(ST_FLAT_ALT);
 }
 
 unsigned int

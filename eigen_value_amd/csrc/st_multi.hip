@@ -122,16 +122,19 @@ comm_wait(const ncclComm_t* comms, int n, const int* ranks, const int* devs,
 
 // Communicator creation under the deadline.  RCCL 2.27's
 // ncclCommInitRankConfig does not return to its caller while a peer is
-// missing, non-blocking config or not (tools/comm_deadline_probe.cpp,
-// profiles/r04_comm_deadline_probe.log), so the init runs on a helper
-// thread and this thread waits for it at most the deadline.  Past it the
-// call fails with the stalled rank named; any handle RCCL already wrote is
-// aborted from another detached thread (ncclCommAbort may itself wait for
-// the init), and the helper is left behind - the caller is expected to end
-// the job, which is what the deadline is for.
+// missing, non-blocking config or not, and ncclCommGetAsyncError reports
+// ncclSuccess on the half-made handle meanwhile; but the handle is written
+// early, and ncclCommAbort from another thread returns at once and makes
+// the blocked init return an error (tools/comm_deadline_probe.cpp,
+// profiles/r04_comm_deadline_probe.log).  So the init runs on a helper
+// thread, which also completes the non-blocking group job (its state is
+// thread-local to the thread that ended the group: the helper must not
+// exit before the communicators are ready), and this thread waits for it at
+// most the deadline; past it, every handle RCCL wrote is aborted and the
+// helper is given a few seconds to return.
 struct InitJob
 {
-  std::vector<ncclComm_t> comms; // written by RCCL (early, non-blocking config)
+  std::vector<ncclComm_t> comms; // written by RCCL (early)
   ncclResult_t r = ncclInProgress;
   int done = 0; // __atomic
 };
@@ -142,45 +145,63 @@ init_with_deadline(const std::shared_ptr<InitJob>& job,
                    const int* devs, const char* what)
 {
   std::thread([job, body]() {
-    const ncclResult_t r = body(*job);
+    ncclResult_t r = body(*job);
+    // finish an asynchronous init here, in the thread that started it
+    for (bool pending = (r == ncclInProgress); pending;) {
+      pending = false;
+      for (ncclComm_t c : job->comms) {
+        ncclResult_t st = ncclSuccess;
+        if (!c)
+          continue;
+        if (ncclCommGetAsyncError(c, &st) != ncclSuccess)
+          st = ncclInternalError;
+        if (st == ncclInProgress)
+          pending = true;
+        else if (st != ncclSuccess && r == ncclInProgress)
+          r = st;
+      }
+      if (pending)
+        std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+    if (r == ncclInProgress)
+      r = ncclSuccess;
     job->r = r;
     __atomic_store_n(&job->done, 1, __ATOMIC_RELEASE);
   }).detach();
   const double limit = comm_timeout_s();
   const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    if (__atomic_load_n(&job->done, __ATOMIC_ACQUIRE))
-      break;
-    const double el = std::chrono::duration<double>(
-                        std::chrono::steady_clock::now() - t0)
-                        .count();
+  auto elapsed = [&t0]() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0)
+      .count();
+  };
+  while (!__atomic_load_n(&job->done, __ATOMIC_ACQUIRE)) {
+    const double el = elapsed();
     if (el > limit) {
-      const int n = (int)job->comms.size();
-      for (int i = 0; i < n; i++) {
+      int aborted = 0;
+      for (size_t i = 0; i < job->comms.size(); i++) {
         ncclComm_t c = __atomic_load_n(&job->comms[i], __ATOMIC_ACQUIRE);
-        if (c)
-          std::thread([c]() { (void)ncclCommAbort(c); }).detach();
+        if (c) {
+          (void)ncclCommAbort(c);
+          aborted++;
+        }
       }
+      // the aborted init returns an error; give the helper a moment
+      const double t_ab = elapsed();
+      while (!__atomic_load_n(&job->done, __ATOMIC_ACQUIRE) && elapsed() < t_ab + 10.0)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
       ::st::set_error("%s: RCCL rank %d (device %d) still in progress after "
                       "%.1f s (deadline %.1f s, ST_COMM_TIMEOUT_S / "
-                      "st_set_comm_timeout): ncclCommInitRankConfig did not "
-                      "return - a peer did not arrive; communicator aborted",
-                      what, ranks[0], devs[0], el, limit);
+                      "st_set_comm_timeout): a peer did not arrive; %d "
+                      "communicator(s) aborted",
+                      what, ranks[0], devs[0], el, limit, aborted);
       return -1;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(500));
   }
-  // returned: it may still be finishing asynchronously (ncclInProgress)
-  if (job->r != ncclSuccess && job->r != ncclInProgress) {
+  if (job->r != ncclSuccess) {
     ::st::set_error("%s: ncclCommInitRankConfig (RCCL rank %d, device %d) "
                     "failed: %s",
                     what, ranks[0], devs[0], ncclGetErrorString(job->r));
-    for (ncclComm_t c : job->comms)
-      if (c)
-        (void)ncclCommAbort(c);
-    return -1;
-  }
-  if (comm_wait(job->comms.data(), (int)job->comms.size(), ranks, devs, what)) {
     for (ncclComm_t c : job->comms)
       if (c)
         (void)ncclCommAbort(c);

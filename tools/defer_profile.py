@@ -251,7 +251,7 @@ def np_of(name):
     return int(m.group(1).split(",")[11])
 
 
-def summarise(path, n, elem, m, workload, events=None, launches=None, rows=None):
+def summarise(path, n, elem, m, workload, events=None, launches=None, block_rows=None):
     """Per-NP averages of a kernel trace.  `launches`: also write the
     deferred launches themselves (kernel, NP, start, duration; one row per
     launch, in trace order) to this CSV - the trimmed trace that a committed
@@ -288,7 +288,7 @@ def summarise(path, n, elem, m, workload, events=None, launches=None, rows=None)
                 w.writerow([kind, pos, int(r["Start_Timestamp"]) - t0,
                             int(r["End_Timestamp"]) - int(r["Start_Timestamp"]),
                             r["Kernel_Name"][:160]])
-    nb = (rows or n) * n * elem     # rows: a rank block's (--rank-block)
+    nb = (block_rows or n) * n * elem     # a rank block (--rank-block): its rows
     avg = lambda x: sum(x) / len(x)  # noqa: E731
     # the steady state: the first store cycles of a trace run cold (the
     # first storing launch 3.17 ms against 2.82 later at 32768^2 fp64), which

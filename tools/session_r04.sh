@@ -33,6 +33,17 @@ l2)
     run l2_tcp_every_${N} 180 rocprofv3 --pmc TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TOTAL_ACCESSES_sum --output-format csv -d $D/tcp_every -o run -- python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype f64 --every-ab 0 --steps 8 --passes 1
     python3 tools/sq_counters.py $D/tcc_defer/run_counter_collection.csv $D/tcp_defer/run_counter_collection.csv $D/tcc_every/run_counter_collection.csv $D/tcp_every/run_counter_collection.csv --json=$O/r04_l2_random${N}_p${P}_f64.json
   done ;;
+storeab)
+  # the cached fp64 storing round (5 pending) on the weak-scaled rank blocks:
+  # rows x piece tile (probe builds, tools/defer_shape_probe.sh) x workgroup cap
+  for W in "16384 4" "11648 2" "23040 8" "8192 0"; do
+    set -- $W; N=$1; P=$2
+    for V in default s5r4 s5t0 s5t16; do
+      L=eigen_value_amd/lib/variants/$V/libsimilarity_transform.so; [ $V = default ] && L=eigen_value_amd/lib/libsimilarity_transform.so
+      EIGEN_VALUE_LIB=$L run storeab_h${N}_p${P}_$V 240 python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --cycles 40 --passes 5 --caps-ab "0,4,4,3,3,0,3;0,4,4,3,3,0,2;0,4,4,3,3,0,4;0,4,4,3,3,0,0" --ab-json $O/r04_storeab_h${N}_p${P}_$V.json
+      grep "median" $O/storeab_h${N}_p${P}_$V.log | sed "s/^/$V /"
+    done
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 esac; done
