@@ -570,14 +570,19 @@ def rank_block_legs(sharded, torch, cases, kind, steps, warmup, representative):
         if representative:
             r["frac"] = round(rate(by, fused) / HBM_PEAK_GBS, 4)
         if sh.deferred_writes:
-            # as deferred_leg: from a fresh A_0 (the every-round passes above
-            # shrank the off-block columns), ~60 ms of whole store cycles,
-            # three passes, the median (round 3 timed 4 cycles once, which
-            # read 7 % above the A/B tool's figure for the P = 4 block)
-            sh.load(kind, seed=0)
+            # ~60 ms of whole store cycles, three passes, the median, each
+            # pass from a fresh A_0 (a block timed alone holds the other
+            # ranks' row sums at 1.0, so its off-block columns shrink every
+            # round and the memory-side cache streams the decayed values
+            # faster or slower: round 4's passes without the reload read
+            # 0.1015 / 0.1039 / 0.1040 ms on the P = 4 block; round 3 timed 4
+            # cycles once, 7 % above the A/B tool's figure)
             cycles = max(3, int(round(60.0 / max(el / steps * 1e3, 1e-3) / 6)))
-            runs = sorted((timed_deferred(sh, cycles, 2 if i == 0 else 0, torch, None, 1)
-                           for i in range(3)), key=lambda x: x[1])
+
+            def one_pass():
+                sh.load(kind, seed=0)
+                return timed_deferred(sh, cycles, 1, torch, None, 1)
+            runs = sorted((one_pass() for _ in range(3)), key=lambda x: x[1])
             _, ev_d, m = runs[1]
             by_d = (m + 1.0) / m * p.nrows * n * 8
             r["deferred_writes"] = {"stores_every": m, "cycles": cycles,

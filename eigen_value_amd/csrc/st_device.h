@@ -242,6 +242,16 @@ ld(const V* p)
 // profiles/r02_flat_map_rowload_*.log): 15-30 % SLOWER on non-temporal
 // fp64 blocks with pending rounds (32768^2, NP = 1: 1.62 vs 1.33 ms), equal
 // elsewhere, so the library keeps scalar row loads.
+// Probe-only forms of k_flat, compiled only into the tools' sweep builds
+// (tools/Makefile passes -DST_PROBE_FORMS=1): FOLD (k_parts folded into the
+// last arriving workgroup of a row group), DS = -1 with pending rounds (the
+// store decided at run time), FlatPending::pc (pieces walked in column
+// blocks) and the gates other than kGatePlain.  The library launches none of
+// them; k_flat refuses them at compile time without the switch.
+#ifndef ST_PROBE_FORMS
+#define ST_PROBE_FORMS 0
+#endif
+
 #ifndef ST_ROW_VLOAD
 #define ST_ROW_VLOAD 0
 #endif
@@ -1008,7 +1018,10 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
   // group folds round k-1's stats, nothing is stored; k_mparts finishes
   // s_k and v_{k-1}
-  static_assert(!MF || (FS && NP < 0 && SPLIT == 0), "MF: the fused-stats unsplit round");
+  static_assert(!MF || (FS && NP < 0 && SPLIT == 0 && GATE != kGateSpec),
+                "MF: the fused-stats unsplit round (gated on k - 1)");
+  static_assert(ST_PROBE_FORMS || (!FOLD && (NP < 0 || DS >= 0) && GATE == kGatePlain),
+                "probe-only k_flat form: tools builds only (-DST_PROBE_FORMS=1)");
   // the matrix-free launch k evaluates round k - 1 (gated once end <= k - 1)
   const uint32_t kr = MF ? k - 1 : k;
   if constexpr (GATE != kGateSpec) {
@@ -1059,7 +1072,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     // block's row groups tiled over one column block before the next
     const uint32_t pt = pend.pt, ng = (nrows + R - 1) / R;
     uint32_t bb = b, w = ppr, pb = 0;
-    if (pend.pc != 0 && pend.pc < ppr) { // uniform
+    if (ST_PROBE_FORMS && pend.pc != 0 && pend.pc < ppr) { // uniform
       const uint32_t cb = b / (ng * pend.pc);
       pb = cb * pend.pc;
       bb = b - cb * (ng * pend.pc);

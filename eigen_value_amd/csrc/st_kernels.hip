@@ -36,7 +36,7 @@
 #define ST_DEFER_STORE_R8_CACHED 1
 #endif
 #ifndef ST_DEFER_TS5_CACHED // its piece tile (row groups; 0 = row-major)
-#define ST_DEFER_TS5_CACHED 4u
+#define ST_DEFER_TS5_CACHED 16u
 #endif
 #ifndef ST_FLAT_ALT // the flat launches' odd-round order (2 = reversed per XCD, 0 = none)
 #define ST_FLAT_ALT 2
@@ -45,7 +45,7 @@
   (ST_DPP_NOINIT == 1 && ST_ROW_VLOAD == 0 && ST_FLAT_UNMASKED == 1 &&         \
    ST_DEFER_STORE_NT == 0 && ST_EVERY_CACHED_R1 == 1 &&                        \
    ST_DEFER_R0_CACHED == 1 && ST_DEFER_PT0_CACHED == 4 &&                      \
-   ST_DEFER_STORE_R8_CACHED == 1 && ST_DEFER_TS5_CACHED == 4 && ST_FLAT_ALT == 2)
+   ST_DEFER_STORE_R8_CACHED == 1 && ST_DEFER_TS5_CACHED == 16 && ST_FLAT_ALT == 2)
 #ifndef ST_PROBES
 static_assert(ST_PROBES_DEFAULT,
               "A/B probe switch set in a library build (use -DST_PROBES=1)");
@@ -926,8 +926,11 @@ constexpr int kCapStore = 6;
 std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   // fp32: cached, non-temporal
   { { 0, 0, 0, 0, 0, 0, 0 }, { 0, 6, 5, 4, 5, 0, 3 } },
-  // fp64: cached, non-temporal
-  { { 0, 4, 4, 3, 3, 0, 3 }, { 0, 5, 4, 4, 4, 0, 3 } },
+  // fp64: cached, non-temporal (the cached storing round uncapped since
+  // round 4: caps 0 / 3 / 4 tie within 0.1 % on 8192^2 and the three
+  // weak-scaled rank blocks once it is tiled by 16, 2 loses 1-2 %,
+  // profiles/r04_storeab_*_s5t16.json)
+  { { 0, 4, 4, 3, 3, 0, 0 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
 
@@ -1059,9 +1062,16 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
   constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
   // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
   // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
-  // cached fp64 blocks: 8 rows tiled by 4 for the storing round with 5
-  // pending (8192^2 0.160 vs 0.165 ms, the P = 8 block level;
-  // profiles/r02_flat_map_r8_f64_cached_store5.log)
+  // cached fp64 blocks: 8 rows for the storing round with 5 pending
+  // (8192^2 0.160 vs 0.165 ms, the P = 8 block level;
+  // profiles/r02_flat_map_r8_f64_cached_store5.log), tiled by 16 row groups
+  // (round 4: the solve loop over whole store cycles, 5 interleaved passes,
+  // probe builds of 0 / 4 / 16, profiles/r04_storeab_*.json, ms per round,
+  // tile 4 vs 16: the weak-scaled P = 4 block 4096 x 16384 0.1042 vs 0.0983
+  // - its storing launch had taken 0.2016 ms against 0.1644 at 8192^2,
+  // profiles/r04_defer_cycle_hilbert*_p*_f64.json - P = 2 0.1003 vs 0.0992,
+  // P = 8 0.1000 vs 0.1002, 8192^2 0.0953 vs 0.0944; 4 rows lose on all but
+  // P = 4)
   constexpr bool kS8 = !NT && sizeof(T) == 8 && ST_DEFER_STORE_R8_CACHED;
   constexpr int kRS = NT ? 8 : 4;
   constexpr int kRS5 = kS8 ? 8 : kRS;

@@ -46,5 +46,9 @@ storeab)
   done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
+prof)
+  run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu
+  cp $O/prof/run_kernel_stats.csv $O/r04_bench_default_${S:-s}_kernel_stats.csv ;;
+smoke) run smoke 300 python -c 'import __graft_entry__ as g; g.smoke()' ;;
 esac; done
 echo "== session done"
