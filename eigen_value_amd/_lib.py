@@ -54,6 +54,30 @@ class st_stats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_ if k != "reserved"}
 
 
+class st_launch_policy(ctypes.Structure):
+    """include/similarity_transform.h st_launch_policy."""
+    _fields_ = [("kernel", ctypes.c_int), ("rows", ctypes.c_int), ("tile", ctypes.c_uint),
+                ("cap", ctypes.c_uint), ("grid", ctypes.c_uint), ("piece_bytes", ctypes.c_uint),
+                ("load_nt", ctypes.c_int), ("store_nt", ctypes.c_int), ("alt", ctypes.c_int)]
+
+
+ST_FORM_ROUND, ST_FORM_DEFER_READ, ST_FORM_DEFER_STORE, ST_FORM_MFREE = 0, 1, 2, 3
+KERNEL_NAMES = {0: "k_round", 1: "k_flat", 2: "k_flat<NP>", 3: "k_mfree"}
+
+
+def launch_policy(dtype: str, nrows: int, ncols: int, form: int, npend: int = 0) -> dict:
+    """What the solve loops launch for an nrows x ncols block
+    (st_launch_policy_query): kernel, rows per workgroup / group, piece
+    tile, workgroups-per-CU cap, grid cap, piece bytes, cache policy."""
+    L = load()
+    out = st_launch_policy()
+    check(L.st_launch_policy_query(1 if dtype == "f64" else 0, nrows, ncols, form, npend,
+                                   ctypes.byref(out)), "st_launch_policy_query")
+    d = {f: getattr(out, f) for f, _ in st_launch_policy._fields_}
+    d["kernel"] = KERNEL_NAMES[d["kernel"]]
+    return d
+
+
 class st_state(ctypes.Structure):
     _fields_ = [("done", ctypes.c_uint32),
                 ("round", ctypes.c_uint32),
@@ -205,6 +229,8 @@ def _declare(L: ctypes.CDLL) -> None:
     for sfx in ("f32", "f64"):
         getattr(L, f"st_allgather_{sfx}").argtypes = [P, P, P, u64, P]
         getattr(L, f"st_allgather_{sfx}").restype = i32
+    L.st_launch_policy_query.argtypes = [i32, u32, u32, i32, u32, P]
+    L.st_launch_policy_query.restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32
 

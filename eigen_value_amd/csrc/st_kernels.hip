@@ -10,6 +10,8 @@
 //   generators / fill           : grid-stride, 256-thread workgroups
 
 #include <hip/hip_runtime.h>
+
+#include <cstring>
 #include <stdint.h>
 
 #include <atomic>
@@ -1024,6 +1026,46 @@ defer_lds(uint32_t slot)
 //                     2.852 vs 2.931 ms, 8192 x 65536 1.434 vs 1.481)
 // (the every-round flat round has its own shapes: kFlatEveryRows /
 // flat_every_tile above)
+// rows per workgroup and piece tile (row groups, 0 = row-major) of a
+// deferred round, by pending count and store: the table above, in one place
+// for the launcher (template arguments) and st_launch_policy (tests and the
+// pinned map, tests/golden/launch_policy.json)
+template <typename T, bool NT>
+constexpr int
+defer_rows(int np, bool store)
+{
+  // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
+  // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
+  // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
+  // row-major (1 row: 18 % slower at 8192^2 fp32,
+  // profiles/r02_flat_map_r1_f32_cached.log)
+  // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
+  // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there); the cached
+  // fp64 store with 5 pending: 8 (below)
+  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  if (store)
+    return np == 0 ? 4
+           : np < 5 ? (NT ? 8 : 4)
+                    : ((kF64C && ST_DEFER_STORE_R8_CACHED) ? 8 : (NT ? 8 : 4));
+  return np == 0 ? (NT ? 2 : kF64C ? ST_DEFER_R0_CACHED : 2)
+         : np == 1 ? 4
+         : np == 2 ? (NT ? 8 : 4) // NP = 2: 1-2 % with 8 rows, non-temporal only
+                   : 8;
+}
+
+template <typename T, bool NT>
+constexpr uint32_t
+defer_tile(int np, bool store)
+{
+  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  if (store)
+    return (np >= 5 && kF64C && ST_DEFER_STORE_R8_CACHED) ? (uint32_t)ST_DEFER_TS5_CACHED
+                                                           : 0u;
+  return np == 0 ? (NT ? 8u : kF64C ? (uint32_t)ST_DEFER_PT0_CACHED : 0u)
+         : np <= 2 ? (NT ? 32u : 16u)
+                   : 16u;
+}
+
 template <typename T, int W, int ORDER, bool NT>
 void
 launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
@@ -1035,69 +1077,49 @@ launch_flat_deferred(T* a, const T* s_cur, const T* inv_cur, T* s_next,
                      hipStream_t stream)
 {
   // the matrix loads' / stores' cache policy turned over where
-  // g_defer_flip says so (vector path only; kF64C: the cached fp64 form)
-  constexpr bool kF64C = !NT && sizeof(T) == 8;
+  // g_defer_flip says so (vector path only)
   constexpr int kV = W > 1 ? 1 : 0;
   const uint32_t fl = kV ? defer_flip<T>(nrows, ncols) : 0u;
 #define ST_NPL(NPV, RV, STV, FLV, PTV, LDS)                                    \
   launch_flat_deferred_np<T, W, ORDER, NT, NPV, RV, STV, (FLV) * kV>(          \
     a, s_cur, inv_cur, s_next, inv_next, part, v, nrows, ncols, row0, eps, k,  \
     max_itr, semantics, st, pend_s, pend_inv, flush, PTV, LDS, stream)
-#define ST_NP(NPV, RV, PTV, LDS)                                               \
-  (((fl >> (NPV)) & 1u) ? ST_NPL(NPV, RV, false, 1, PTV, LDS)                  \
-                        : ST_NPL(NPV, RV, false, 0, PTV, LDS))
-#define ST_NPS(NPV, RV, PTV, LDS)                                              \
+#define ST_NP(NPV, LDS)                                                        \
+  (((fl >> (NPV)) & 1u)                                                        \
+     ? ST_NPL(NPV, (defer_rows<T, NT>(NPV, false)), false, 1,                  \
+              (defer_tile<T, NT>(NPV, false)), LDS)                            \
+     : ST_NPL(NPV, (defer_rows<T, NT>(NPV, false)), false, 0,                  \
+              (defer_tile<T, NT>(NPV, false)), LDS))
+#define ST_NPS1(NPV, FLV, LDS)                                                 \
+  ST_NPL(NPV, (defer_rows<T, NT>(NPV, true)), true, FLV,                       \
+         (defer_tile<T, NT>(NPV, true)), LDS)
+#define ST_NPS(NPV, LDS)                                                       \
   (((fl >> kNtStoreBit) & 1u)                                                  \
-     ? (((fl >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, 3, PTV, LDS)          \
-                                 : ST_NPL(NPV, RV, true, 2, PTV, LDS))         \
-     : (((fl >> kCapStore) & 1u) ? ST_NPL(NPV, RV, true, 1, PTV, LDS)          \
-                                 : ST_NPL(NPV, RV, true, 0, PTV, LDS)))
-  // NP = 0 on cached fp64 blocks: 1 row, tiles of 4 (the solve loop 0.3 -
-  // 0.7 % faster per round at 8192^2 / 10240^2 / 12288^2,
-  // profiles/r02_defer_cycle_ab_np0_cached.log); fp32 keeps 2 rows,
-  // row-major (1 row: 18 % slower at 8192^2 fp32,
-  // profiles/r02_flat_map_r1_f32_cached.log)
-  constexpr int kR0 = NT ? 2 : kF64C ? ST_DEFER_R0_CACHED : 2;
-  constexpr uint32_t kTile0 = NT ? 8u : kF64C ? ST_DEFER_PT0_CACHED : 0u;
-  constexpr uint32_t kTile12 = NT ? 32u : 16u, kTile34 = 16u;
-  // stores with pending rounds: 8 rows on non-temporal blocks, 4 cached
-  // (8192^2 fp32 and the P = 8 block lose 3-5 % with 8 there)
-  // cached fp64 blocks: 8 rows for the storing round with 5 pending
-  // (8192^2 0.160 vs 0.165 ms, the P = 8 block level;
-  // profiles/r02_flat_map_r8_f64_cached_store5.log), tiled by 16 row groups
-  // (round 4: the solve loop over whole store cycles, 5 interleaved passes,
-  // probe builds of 0 / 4 / 16, profiles/r04_storeab_*.json, ms per round,
-  // tile 4 vs 16: the weak-scaled P = 4 block 4096 x 16384 0.1042 vs 0.0983
-  // - its storing launch had taken 0.2016 ms against 0.1644 at 8192^2,
-  // profiles/r04_defer_cycle_hilbert*_p*_f64.json - P = 2 0.1003 vs 0.0992,
-  // P = 8 0.1000 vs 0.1002, 8192^2 0.0953 vs 0.0944; 4 rows lose on all but
-  // P = 4)
-  constexpr bool kS8 = !NT && sizeof(T) == 8 && ST_DEFER_STORE_R8_CACHED;
-  constexpr int kRS = NT ? 8 : 4;
-  constexpr int kRS5 = kS8 ? 8 : kRS;
-  constexpr uint32_t kTileS5 = kS8 ? ST_DEFER_TS5_CACHED : 0u;
-  constexpr int kR2 = NT ? 8 : 4; // NP = 2: 1-2 % with 8 rows, non-temporal only
+     ? (((fl >> kCapStore) & 1u) ? ST_NPS1(NPV, 3, LDS) : ST_NPS1(NPV, 2, LDS)) \
+     : (((fl >> kCapStore) & 1u) ? ST_NPS1(NPV, 1, LDS) : ST_NPS1(NPV, 0, LDS)))
   static_assert(kDeferRoundsMax == 6, "one case per pending count below");
+  // shapes: defer_rows / defer_tile; caps: g_defer_caps
   if (store) {
     const uint32_t lds = defer_lds<T, NT>(kCapStore);
     switch (npend) {
-    case 0: ST_NPS(0, 4, 0u, lds); break;
-    case 1: ST_NPS(1, kRS, 0u, lds); break;
-    case 2: ST_NPS(2, kRS, 0u, lds); break;
-    case 3: ST_NPS(3, kRS, 0u, lds); break;
-    case 4: ST_NPS(4, kRS, 0u, lds); break;
-    default: ST_NPS(5, kRS5, kTileS5, lds); break;
+    case 0: ST_NPS(0, lds); break;
+    case 1: ST_NPS(1, lds); break;
+    case 2: ST_NPS(2, lds); break;
+    case 3: ST_NPS(3, lds); break;
+    case 4: ST_NPS(4, lds); break;
+    default: ST_NPS(5, lds); break;
     }
   } else {
     const uint32_t lds = defer_lds<T, NT>(npend < 5 ? npend : 4);
     switch (npend) {
-    case 0: ST_NP(0, kR0, kTile0, lds); break;
-    case 1: ST_NP(1, 4, kTile12, lds); break;
-    case 2: ST_NP(2, kR2, kTile12, lds); break;
-    case 3: ST_NP(3, 8, kTile34, lds); break;
-    default: ST_NP(4, 8, kTile34, lds); break;
+    case 0: ST_NP(0, lds); break;
+    case 1: ST_NP(1, lds); break;
+    case 2: ST_NP(2, lds); break;
+    case 3: ST_NP(3, lds); break;
+    default: ST_NP(4, lds); break;
     }
   }
+#undef ST_NPS1
 #undef ST_NP
 #undef ST_NPS
 #undef ST_NPL
@@ -1532,6 +1554,82 @@ template int launch_mfree<double>(const double*, const double*, double*,
 template int launch_fill<float>(float*, uint64_t, float, hipStream_t);
 template int launch_fill<double>(double*, uint64_t, double, hipStream_t);
 
+// ---- the launch policy, as one map (st_launch_policy) ---------------------
+// What the solve loops launch for a block, read from the same functions and
+// tables the launchers above use (round_shape / mfree_shape, kFlatEveryRows
+// / flat_every_tile / g_every_cache / g_every_caps, defer_rows / defer_tile
+// / g_defer_flip / g_defer_caps), so the pinned map
+// (tests/golden/launch_policy.json, tools/launch_policy_table.py) changes
+// whenever a launch does.  Vector path (ncols a multiple of 16 / b).
+namespace {
+template <typename T, bool NT>
+int
+policy_flat(uint32_t nrows, uint32_t ncols, int form, uint32_t np,
+            st_launch_policy* o)
+{
+  constexpr int W = 16 / sizeof(T);
+  o->piece_bytes = (uint32_t)(kBlock * W * kFlatU<T, W, NT> * sizeof(T));
+  o->grid = 0;
+  o->alt = kFlatAlt != 0;
+  const uint32_t cls = every_cache_class(block_bytes(nrows, ncols, sizeof(T)));
+  if (form == ST_FORM_ROUND) {
+    const uint32_t pol = g_every_cache[cls].load(std::memory_order_relaxed);
+    o->kernel = ST_KERNEL_FLAT;
+    o->rows = kFlatEveryRows<T, NT>;
+    o->tile = flat_every_tile<T, NT>(nrows, ncols);
+    o->cap = g_every_caps[cls].load(std::memory_order_relaxed);
+    o->load_nt = NT != ((pol & 1u) != 0);
+    o->store_nt = NT != ((pol & 2u) != 0);
+    return 0;
+  }
+  const bool store = form == ST_FORM_DEFER_STORE;
+  ST_REQUIRE(np < kDeferRoundsMax && (store || np + 1 < kDeferRoundsMax),
+             "st_launch_policy: %u pending rounds %s", np,
+             store ? "(at most 5)" : "without a store (at most 4)");
+  const uint32_t fl = defer_flip<T>(nrows, ncols);
+  o->kernel = ST_KERNEL_FLAT_DEFERRED;
+  o->rows = defer_rows<T, NT>((int)np, store);
+  o->tile = defer_tile<T, NT>((int)np, store);
+  o->cap = g_defer_caps[sizeof(T) == 8][NT][store ? kCapStore : (np < 5 ? np : 4)].load(
+    std::memory_order_relaxed);
+  o->load_nt = NT != (((fl >> (store ? (uint32_t)kCapStore : np)) & 1u) != 0);
+  o->store_nt = store ? (int)((NT || ST_DEFER_STORE_NT) != (((fl >> kNtStoreBit) & 1u) != 0))
+                      : -1;
+  return 0;
+}
+
+template <typename T>
+int
+policy(uint32_t nrows, uint32_t ncols, int form, uint32_t np, st_launch_policy* o)
+{
+  std::memset(o, 0, sizeof(*o));
+  if (form == ST_FORM_MFREE) {
+    const Shape sh = mfree_shape(nrows, ncols, sizeof(T));
+    o->kernel = ST_KERNEL_MFREE;
+    o->rows = sh.rows;
+    o->grid = sh.grid;
+    o->load_nt = sh.nt;
+    o->store_nt = -1;
+    o->alt = 1;
+    return 0;
+  }
+  if (!round_flat_pays(nrows, ncols, sizeof(T))) {
+    ST_REQUIRE(form == ST_FORM_ROUND,
+               "st_launch_policy: deferred writes need the flat round (>= 144 MiB)");
+    const Shape sh = round_shape(nrows, ncols, sizeof(T));
+    o->kernel = ST_KERNEL_ROUND;
+    o->rows = sh.rows;
+    o->grid = sh.grid;
+    o->load_nt = o->store_nt = sh.nt;
+    o->alt = 1;
+    return 0;
+  }
+  return flat_round_nt(nrows, ncols, sizeof(T))
+           ? policy_flat<T, true>(nrows, ncols, form, np, o)
+           : policy_flat<T, false>(nrows, ncols, form, np, o);
+}
+} // namespace
+
 } // namespace st
 
 // ---------------------------------------------------------------------------
@@ -1748,6 +1846,20 @@ st_round_split_flat_scratch(unsigned int nrows, unsigned int ncols,
   if (col1 < col0)
     return 0;
   return st::split_flat_scratch_elems(nrows, ncols, col0, col1);
+}
+
+int
+st_launch_policy_query(int dtype, unsigned int nrows, unsigned int ncols, int form,
+                       unsigned int npend, st_launch_policy* out)
+{
+  st::clear_error();
+  ST_REQUIRE(out, "st_launch_policy: null output");
+  ST_REQUIRE(dtype == 0 || dtype == 1, "st_launch_policy: dtype 0 (fp32) or 1 (fp64)");
+  ST_REQUIRE(nrows > 0 && ncols > 0 && ncols % (dtype == 1 ? 2u : 4u) == 0,
+             "st_launch_policy: a block of whole 16-byte chunks per row");
+  ST_REQUIRE(form >= ST_FORM_ROUND && form <= ST_FORM_MFREE, "st_launch_policy: form 0..3");
+  return dtype == 1 ? st::policy<double>(nrows, ncols, form, npend, out)
+                    : st::policy<float>(nrows, ncols, form, npend, out);
 }
 
 int

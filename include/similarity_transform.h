@@ -405,6 +405,36 @@ int st_set_every_tile(unsigned int size_class, unsigned int tile);
  * on bad arguments. */
 int st_set_mfree_shape(unsigned int shape);
 
+/* The launch policy, as one map: what the solve loops launch for an
+ * nrows x ncols block of `dtype` (0 fp32, 1 fp64; vector path, ncols a
+ * multiple of 16 / sizeof element) in `form`, with `npend` pending rounds for
+ * the deferred forms - read from the same shape functions and tables the
+ * launchers use (st_kernels.hip), so tests/golden/launch_policy.json pins
+ * every launch shape and cache policy.  Returns 0 or negative. */
+#define ST_FORM_ROUND 0       /* a round that stores A (bench step; the
+                                 solve's round below 144 MiB)                 */
+#define ST_FORM_DEFER_READ 1  /* deferred writes: a read-only round          */
+#define ST_FORM_DEFER_STORE 2 /* deferred writes: the storing round          */
+#define ST_FORM_MFREE 3       /* the matrix-free round                        */
+#define ST_KERNEL_ROUND 0     /* k_round: grid-stride row groups              */
+#define ST_KERNEL_FLAT 1      /* k_flat + k_parts, storing every round        */
+#define ST_KERNEL_FLAT_DEFERRED 2 /* k_flat<NP> + k_parts                     */
+#define ST_KERNEL_MFREE 3     /* k_mfree                                      */
+typedef struct st_launch_policy
+{
+  int kernel;               /* ST_KERNEL_*                                    */
+  int rows;                 /* rows per workgroup (flat) or per row group     */
+  unsigned int tile;        /* flat: row groups per piece tile, 0 = row-major */
+  unsigned int cap;         /* workgroups per CU (dynamic LDS), 0 = uncapped  */
+  unsigned int grid;        /* grid-stride kernels: workgroup count cap       */
+  unsigned int piece_bytes; /* flat: bytes of a row per workgroup piece       */
+  int load_nt;              /* matrix loads non-temporal                      */
+  int store_nt;             /* matrix stores non-temporal, -1 = no stores     */
+  int alt;                  /* odd rounds walk the block in reverse           */
+} st_launch_policy;
+int st_launch_policy_query(int dtype, unsigned int nrows, unsigned int ncols,
+                           int form, unsigned int npend, st_launch_policy* out);
+
 /* The size class st_set_every_cache indexes for an nrows x ncols block
  * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
 int st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype);

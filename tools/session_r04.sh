@@ -44,6 +44,15 @@ storeab)
       grep "median" $O/storeab_h${N}_p${P}_$V.log | sed "s/^/$V /"
     done
   done ;;
+capsdrop)
+  # the workgroup caps of the read-only deferred rounds against none (the
+  # storing round keeps its own): entries inside the box-to-box spread go
+  run capsdrop_f64_8192 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --cycles 40 --passes 7 --caps-ab "0,4,4,3,3,0,0;0,0,0,0,0,0,0" --ab-json $O/r04_capsdrop_hilbert8192_f64.json
+  run capsdrop_f64_8192_p8 300 python3 tools/defer_profile.py --kind hilbert --n 23040 --rank-block 8 --dtype f64 --cycles 40 --passes 7 --caps-ab "0,4,4,3,3,0,0;0,0,0,0,0,0,0" --ab-json $O/r04_capsdrop_hilbert23040_p8_f64.json
+  run capsdrop_f64_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f64 --cycles 6 --passes 7 --caps-ab "0,5,4,4,4,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random32768_f64.json
+  run capsdrop_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 7 --caps-ab "0,5,4,4,4,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random65536_p8_f64.json
+  run capsdrop_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 7 --caps-ab "0,6,5,4,5,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random32768_f32.json
+  grep -h median $O/capsdrop_*.log ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
