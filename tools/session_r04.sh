@@ -53,6 +53,7 @@ capsdrop)
   run capsdrop_f64_65536_p8 300 python3 tools/defer_profile.py --kind random --n 65536 --rank-block 8 --dtype f64 --cycles 6 --passes 7 --caps-ab "0,5,4,4,4,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random65536_p8_f64.json
   run capsdrop_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 7 --caps-ab "0,6,5,4,5,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random32768_f32.json
   grep -h median $O/capsdrop_*.log ;;
+samegpu) run rccl_same_gpu 150 python3 tools/rccl_same_gpu_probe.py --ranks 2 --timeout 30 ; cat $O/rccl_same_gpu.log ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
