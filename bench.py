@@ -1050,15 +1050,51 @@ def main():
     value = bytes_round_total * args.steps / el / 1e9
     achieved = rate(bytes_round_local, fused_ms)
     progress(f"{workload}: {args.steps} timed rounds, {el / args.steps * 1e3:.4f} ms per round")
+    # ---- N > 1: the same rounds with the exchange overlapped --------------
+    # (split launch: local columns while the all-gather runs on a second
+    # stream, sharded.py overlap=True).  Both schedules compute the same
+    # round (A, v, m and the stop decisions bitwise; s to rounding where a
+    # piece straddles the local columns); the line's `value` is the faster
+    # of the two on this machine and the other is reported beside it
+    # (`exchange_schedule`; --overlap forces the overlapped one)
+    overlap_leg = None
+    schedule = "overlapped" if args.overlap else "plain"
+    if world > 1 and not args.overlap and not args.no_overlap_leg:
+        ov = sharded.ShardedSimilarityTransform(n, dt, overlap=True)
+        ov.load(args.kind)
+        lam_ov, _, it_ov, _ = ov.solve(eps=1e-3, max_itr=1000, batch=1)
+        ov.load(args.kind)
+        el_ov, k_ov = timed_rounds(ov, args.steps, args.warmup, torch, dist, world)
+        overlap_leg = {"ms_per_iteration": round(el_ov / args.steps * 1e3, 5),
+                       "value": round(bytes_round_total * args.steps / el_ov / 1e9, 2),
+                       "round_ms_avg": round(k_ov, 5),
+                       "solve_iter_count": it_ov,
+                       "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
+        ov.close()
+        del ov
+        progress(f"overlapped-exchange leg done: {overlap_leg['ms_per_iteration']} ms per round "
+                 f"(plain {el / args.steps * 1e3:.5f})")
+        if el_ov < el and it_ov == iters:
+            overlap_leg = {"schedule": "plain (all-gather after the round)",
+                           "ms_per_iteration": round(el / args.steps * 1e3, 5),
+                           "value": round(value, 2), "round_ms_avg": round(fused_ms, 5),
+                           "solve_iter_count": iters}
+            el, fused_ms, schedule = el_ov, k_ov, "overlapped"
+            value = bytes_round_total * args.steps / el / 1e9
+            achieved = rate(bytes_round_local, fused_ms)
+        else:
+            overlap_leg["schedule"] = "overlapped (split round, all-gather on a second stream)"
+
+    use_overlap = schedule == "overlapped"
     flat_pays = dev.flat_round_pays(p.nrows, n, dt)
-    flat = (not args.overlap) and flat_pays
+    flat = (not use_overlap) and flat_pays
     traffic = load_traffic(workload, "k_flat" if flat else "k_round")
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None if traffic is None else traffic[0],
                 "kernel": (("flat split: k_flat local + k_flat remote + k_parts" if flat_pays
                             else "k_round_split local + remote") + " (overlapped exchange)"
-                           if args.overlap
+                           if use_overlap
                            else "flat round: k_flat + k_parts" if flat
                            else "k_round (fused stats + scale + row-sum)"),
                 "fused_ms_avg": round(fused_ms, 5),
@@ -1078,25 +1114,6 @@ def main():
                     "collective": ("library RCCL communicator (st_allgather)" if sh.rccl
                                    else "torch.distributed all_gather")}
         exchange["rccl_ranks"] = sh.rccl.info()["nranks"] if sh.rccl is not None else None
-
-    # ---- N > 1: the same rounds with the exchange overlapped --------------
-    # (split launch: local columns while the all-gather runs on a second
-    # stream, sharded.py overlap=True); reported beside the headline
-    overlap_leg = None
-    if world > 1 and not args.overlap and not args.no_overlap_leg:
-        ov = sharded.ShardedSimilarityTransform(n, dt, overlap=True)
-        ov.load(args.kind)
-        lam_ov, _, it_ov, _ = ov.solve(eps=1e-3, max_itr=1000, batch=1)
-        ov.load(args.kind)
-        el_ov, k_ov = timed_rounds(ov, args.steps, args.warmup, torch, dist, world)
-        overlap_leg = {"ms_per_iteration": round(el_ov / args.steps * 1e3, 5),
-                       "value": round(bytes_round_total * args.steps / el_ov / 1e9, 2),
-                       "round_ms_avg": round(k_ov, 5),
-                       "solve_iter_count": it_ov,
-                       "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
-        ov.close()
-        del ov
-        progress("overlapped-exchange leg done")
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
@@ -1143,13 +1160,15 @@ def main():
                                           f"row-block sharding over {world} GPU(s), "
                                           + ("strong" if args.strong else "weak") + "-scaled")},
            "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
-    if args.overlap:
+    if use_overlap:
         out["config"]["exchange"] = "overlapped (split round, all-gather on a second stream)"
+    if world > 1:
+        out["config"]["exchange_schedule"] = schedule
     if exchange is not None:
         out["exchange"] = exchange
         out["rccl_ranks"] = exchange["rccl_ranks"]
     if overlap_leg is not None:
-        out["exchange_overlap"] = overlap_leg
+        out["exchange_other_schedule"] = overlap_leg
     if weak_blocks is not None:
         out["weak_rank_blocks"] = weak_blocks
     sh.close()

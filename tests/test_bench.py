@@ -132,7 +132,7 @@ def test_bench_self_spawned_two_ranks_on_one_gpu():
     marked non-representative (no roofline fractions)."""
     out = subprocess.run(
         [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--one-gpu",
-         "--backend", "gloo", "--steps", "5", "--warmup", "1", "--no-overlap-leg"],
+         "--backend", "gloo", "--steps", "5", "--warmup", "1"],
         capture_output=True, text=True, timeout=600, cwd=REPO,
         env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
     assert out.returncode == 0, out.stderr[-4000:]
@@ -146,6 +146,12 @@ def test_bench_self_spawned_two_ranks_on_one_gpu():
     assert c3["solve"]["check"]["iter_count_equal"] is True
     assert c3["solve"]["check"]["eigen_val_rel_err_vs_oracle"] <= 1e-10
     assert d["exchange"]["backend"] == "gloo" and d["rccl_ranks"] is None
+    # both exchange schedules timed; `value` is the faster, the other beside it
+    sched = d["config"]["exchange_schedule"]
+    other = d["exchange_other_schedule"]
+    assert sched in ("plain", "overlapped") and other["schedule"].split()[0] != sched
+    assert other["ms_per_iteration"] >= d["ms_per_step"]
+    assert other["solve_iter_count"] == d["solve"]["iter_count"]
 
 
 @pytest.mark.gpu
