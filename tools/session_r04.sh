@@ -54,6 +54,16 @@ capsdrop)
   run capsdrop_f32_32768 300 python3 tools/defer_profile.py --kind random --n 32768 --dtype f32 --cycles 8 --passes 7 --caps-ab "0,6,5,4,5,0,3;0,0,0,0,0,0,3" --ab-json $O/r04_capsdrop_random32768_f32.json
   grep -h median $O/capsdrop_*.log ;;
 samegpu) run rccl_same_gpu 150 python3 tools/rccl_same_gpu_probe.py --ranks 2 --timeout 30 ; cat $O/rccl_same_gpu.log ;;
+ntstore)
+  # the non-temporal storing round's piece tile (probe builds) x its cap
+  for W in "32768 0 f64 0,5,4,4,4,0" "65536 8 f64 0,5,4,4,4,0" "32768 0 f32 0,6,5,4,5,0"; do
+    set -- $W; N=$1; P=$2; DT=$3; C=$4
+    for V in default tsnt4 tsnt8 tsnt16 tsnt32; do
+      L=eigen_value_amd/lib/variants/$V/libsimilarity_transform.so; [ $V = default ] && L=eigen_value_amd/lib/libsimilarity_transform.so
+      EIGEN_VALUE_LIB=$L run ntstore_r${N}_p${P}_${DT}_$V 240 python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype $DT --cycles 6 --passes 5 --caps-ab "$C,3;$C,0;$C,4" --ab-json $O/r04_ntstore_r${N}_p${P}_${DT}_$V.json
+      grep "median" $O/ntstore_r${N}_p${P}_${DT}_$V.log | sed "s/^/$V /"
+    done
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
