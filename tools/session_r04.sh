@@ -64,6 +64,7 @@ ntstore)
       grep "median" $O/ntstore_r${N}_p${P}_${DT}_$V.log | sed "s/^/$V /"
     done
   done ;;
+gather) run gather_overhead 300 python3 tools/gather_overhead.py; cat $O/gather_overhead.log | grep -v "^RCCL\|^HIP\|^ROCm\|^Host\|^Librccl" ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
