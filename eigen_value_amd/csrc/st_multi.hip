@@ -47,13 +47,15 @@ namespace {
   } while (0)
 
 // ---------------------------------------------------------------------------
-// deadline on every RCCL step that waits for peers.  Communicators are made
-// non-blocking (ncclConfig_t.blocking = 0), so ncclCommInitRankConfig and a
-// group's first collective (its connection setup) return ncclInProgress and
-// this thread polls ncclCommGetAsyncError until they finish or the deadline
-// passes; then the communicators are aborted and the call returns -1 with
-// the stalled rank and device named, instead of hanging in
-// ncclCommInitRank / ncclCommInitAll when a peer never arrives.
+// deadline on every RCCL step that waits for peers (comm_timeout_s).
+// Communicators are non-blocking (ncclConfig_t.blocking = 0): a collective
+// whose connection setup is still running returns ncclInProgress and this
+// thread polls ncclCommGetAsyncError until it is enqueued or the deadline
+// passes (comm_wait / comm_settle).  Creation, which RCCL does not return
+// from while a peer is missing, runs on a helper thread under the same
+// deadline (init_with_deadline).  Past it the communicators are aborted and
+// the call returns -1 with the stalled rank and device named, instead of
+// hanging in ncclCommInitRank / ncclCommInitAll / the first all-gather.
 // ---------------------------------------------------------------------------
 double g_comm_timeout_s = -1.0; // < 0: ST_COMM_TIMEOUT_S or 120 s
 
