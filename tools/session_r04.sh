@@ -65,6 +65,19 @@ ntstore)
     done
   done ;;
 gather) run gather_overhead 300 python3 tools/gather_overhead.py; cat $O/gather_overhead.log | grep -v "^RCCL\|^HIP\|^ROCm\|^Host\|^Librccl" ;;
+pmc)
+  # HBM bytes of the headline launches (separate FETCH_SIZE / WRITE_SIZE
+  # passes, tools/pmc_traffic.py applies the gfx950 x2 FETCH correction)
+  for W in "hilbert 8192 f64 8" "random 32768 f64 8" "random 32768 f32 4"; do
+    set -- $W; K=$1; N=$2; DT=$3; E=$4; D=$O/${K}${N}_${DT}; mkdir -p $D
+    X="--kind $K --n $N --dtype $DT --no-cpu --no-north-star --no-headline"
+    run prof_${K}${N}_${DT} 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py $X
+    run pmcf_${K}${N}_${DT} 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/pmc_fetch -o run -- python3 bench.py $X --steps 20 --warmup 2
+    run pmcw_${K}${N}_${DT} 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/pmc_write -o run -- python3 bench.py $X --steps 20 --warmup 2
+    T=double; [ $DT = f32 ] && T=float
+    python3 tools/pmc_traffic.py --workload ${K}${N}_${DT} --n $N --elem $E --dtype $T --fetch $D/pmc_fetch/run_counter_collection.csv --write $D/pmc_write/run_counter_collection.csv --trace $D/prof/run_kernel_trace.csv --out $O/r04_${K}${N}_${DT}_pmc.json
+    cp $D/prof/run_kernel_stats.csv $O/r04_${K}${N}_${DT}_kernel_stats.csv
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
