@@ -40,9 +40,6 @@
 #ifndef ST_DEFER_TS5_CACHED // its piece tile (row groups; 0 = row-major)
 #define ST_DEFER_TS5_CACHED 16u
 #endif
-#ifndef ST_DEFER_TS_NT // piece tile of the non-temporal storing rounds (0 = row-major)
-#define ST_DEFER_TS_NT 0u
-#endif
 #ifndef ST_FLAT_ALT // the flat launches' odd-round order (2 = reversed per XCD, 0 = none)
 #define ST_FLAT_ALT 2
 #endif
@@ -50,8 +47,7 @@
   (ST_DPP_NOINIT == 1 && ST_ROW_VLOAD == 0 && ST_FLAT_UNMASKED == 1 &&         \
    ST_DEFER_STORE_NT == 0 && ST_EVERY_CACHED_R1 == 1 &&                        \
    ST_DEFER_R0_CACHED == 1 && ST_DEFER_PT0_CACHED == 4 &&                      \
-   ST_DEFER_STORE_R8_CACHED == 1 && ST_DEFER_TS5_CACHED == 16 && ST_DEFER_TS_NT == 0 && \
-   ST_FLAT_ALT == 2)
+   ST_DEFER_STORE_R8_CACHED == 1 && ST_DEFER_TS5_CACHED == 16 && ST_FLAT_ALT == 2)
 #ifndef ST_PROBES
 static_assert(ST_PROBES_DEFAULT,
               "A/B probe switch set in a library build (use -DST_PROBES=1)");
@@ -1062,10 +1058,12 @@ constexpr uint32_t
 defer_tile(int np, bool store)
 {
   constexpr bool kF64C = !NT && sizeof(T) == 8;
+  // storing rounds row-major, but the cached fp64 one with 5 pending (on
+  // non-temporal blocks tiles of 4 ... 32 lose 0.3 - 6 %,
+  // profiles/r04_ntstore_*.json)
   if (store)
-    return NT ? (np > 0 ? (uint32_t)ST_DEFER_TS_NT : 0u)
-           : (np >= 5 && kF64C && ST_DEFER_STORE_R8_CACHED) ? (uint32_t)ST_DEFER_TS5_CACHED
-                                                             : 0u;
+    return (np >= 5 && kF64C && ST_DEFER_STORE_R8_CACHED) ? (uint32_t)ST_DEFER_TS5_CACHED
+                                                           : 0u;
   return np == 0 ? (NT ? 8u : kF64C ? (uint32_t)ST_DEFER_PT0_CACHED : 0u)
          : np <= 2 ? (NT ? 32u : 16u)
                    : 16u;
@@ -1829,8 +1827,7 @@ st_probe_switches(void)
                      " ST_DEFER_PT0_CACHED=" ST_STR(ST_DEFER_PT0_CACHED)
                        " ST_DEFER_STORE_R8_CACHED=" ST_STR(
                          ST_DEFER_STORE_R8_CACHED) " ST_DEFER_TS5_CACHED=" ST_STR(
-                           ST_DEFER_TS5_CACHED) " ST_DEFER_TS_NT=" ST_STR(ST_DEFER_TS_NT)
-                             " ST_FLAT_ALT=" ST_STR(ST_FLAT_ALT);
+                           ST_DEFER_TS5_CACHED) " ST_FLAT_ALT=" ST_STR(ST_FLAT_ALT);
 }
 
 unsigned int
