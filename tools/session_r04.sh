@@ -78,6 +78,11 @@ pmc)
     python3 tools/pmc_traffic.py --workload ${K}${N}_${DT} --n $N --elem $E --dtype $T --fetch $D/pmc_fetch/run_counter_collection.csv --write $D/pmc_write/run_counter_collection.csv --trace $D/prof/run_kernel_trace.csv --out $O/r04_${K}${N}_${DT}_pmc.json
     cp $D/prof/run_kernel_stats.csv $O/r04_${K}${N}_${DT}_kernel_stats.csv
   done ;;
+torchrun8)
+  # the driver's N > 1 launch line, rehearsed: torch.distributed.run with 8
+  # ranks, all on cuda:0 over gloo (--one-gpu: plumbing, not scaling data)
+  run torchrun8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 8 --steps 5 --warmup 1 --backend gloo --one-gpu
+  grep -v "^\[W\|socket.cpp\|amdgpu.ids" $O/torchrun8.log | tail -c 3000 ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
