@@ -83,6 +83,14 @@ torchrun8)
   # ranks, all on cuda:0 over gloo (--one-gpu: plumbing, not scaling data)
   run torchrun8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 8 --steps 5 --warmup 1 --backend gloo --one-gpu
   grep -v "^\[W\|socket.cpp\|amdgpu.ids" $O/torchrun8.log | tail -c 3000 ;;
+ragged)
+  # the weak P = 2 block's ragged last 8 KB piece: rank-0 blocks of P = 2
+  # partitions with whole (11264, 12288) and ragged (11648) 8 KB pieces per row
+  for N in 11648 11264 12288 8192; do
+    P=2; [ $N = 8192 ] && P=0
+    run ragged_h${N}_p${P} 240 python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --every-ab "0;0" --steps 100 --passes 5 --ab-json $O/r04_ragged_h${N}_p${P}.json
+    grep median $O/ragged_h${N}_p${P}.log
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
