@@ -194,3 +194,30 @@ def test_generated_solve_bit_identical(orc, kind, n, dtype, semantics, eps, max_
     assert (r1.iter_count, r1.rounds_evaluated) == (r2.iter_count, r2.rounds_evaluated)
     assert r1.eigen_val == r2.eigen_val
     assert np.array_equal(r1.eigen_vec, r2.eigen_vec)
+
+
+def test_oracle_under_sanitizers(tmp_path):
+    """The checker itself under AddressSanitizer + UndefinedBehaviorSanitizer
+    (SURVEY.md §5): tests/cpp/oracle_sanitize.c drives every oracle entry
+    point across its internal boundaries (pairwise leaves of 128, the
+    8192-element numpy buffer, ragged rows, n = 1, the streaming solve's
+    uneven chunks) and the reference's 3x3 known answer; any report aborts."""
+    import os
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("no gcc")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "oracle_sanitize")
+    subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-fopenmp",
+                    "-ffp-contract=off", "-std=c11", "-Wall", "-Wextra", "-Wno-unknown-pragmas",
+                    os.path.join(repo, "tests", "cpp", "oracle_sanitize.c"),
+                    os.path.join(repo, "oracle", "st_oracle.c"), "-lm", "-o", exe],
+                   check=True, capture_output=True, text=True)
+    env = dict(os.environ, OMP_NUM_THREADS="2")
+    # the environment may preload a library ahead of the ASan runtime
+    env["ASAN_OPTIONS"] = "verify_asan_link_order=0"
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr[-3000:]
+    assert "clean" in out.stdout
