@@ -1,0 +1,29 @@
+#!/bin/bash
+# The library's HOST code under AddressSanitizer + UndefinedBehaviorSanitizer
+# (-Xarch_host only: device code is built as shipped; GPU ASan is not
+# available on the pool), driven by tests/cpp/capi_sanitize.c.
+#   bash tools/host_asan.sh build   # here (about 2.5 min: st_kernels.hip)
+#   bash tools/host_asan.sh run     # here (argument / policy paths) or on a
+#                                   # GPU box (also the device solve paths)
+set -e
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+D=$ROOT/tools/asan
+if [ "${1:-run}" = build ]; then
+  mkdir -p $D
+  FL="--offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off -I$ROOT/include -I$ROOT/eigen_value_amd/csrc"
+  SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
+  for f in st_kernels st_solve st_multi; do
+    /opt/rocm/bin/hipcc $FL $SAN -c $ROOT/eigen_value_amd/csrc/$f.hip -o $D/$f.o &
+  done
+  wait
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $SAN -o $D/libsimilarity_transform.so \
+    $D/st_kernels.o $D/st_solve.o $D/st_multi.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+  rm -f $D/*.o
+  /opt/rocm/lib/llvm/bin/clang -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
+    -I$ROOT/include $ROOT/tests/cpp/capi_sanitize.c -L$D -lsimilarity_transform \
+    -Wl,-rpath,'$ORIGIN' -o $D/capi_sanitize
+  echo "built $D/capi_sanitize"
+else
+  # verify_asan_link_order=0: the environment may preload a library first
+  ASAN_OPTIONS=verify_asan_link_order=0:detect_leaks=1 $D/capi_sanitize
+fi
