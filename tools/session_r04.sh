@@ -92,6 +92,14 @@ ragged)
     grep median $O/ragged_h${N}_p${P}.log
   done ;;
 hostasan) run host_asan 300 bash tools/host_asan.sh run; tail -40 $O/host_asan.log | grep -v "^$" | tail -30 ;;
+everyr2)
+  # the every-round cached launch (the headline): 1 row (shipped) vs 2 rows
+  # per workgroup (probe build), each under workgroup caps and piece tiles
+  for V in default er2; do
+    L=eigen_value_amd/lib/variants/$V/libsimilarity_transform.so; [ $V = default ] && L=eigen_value_amd/lib/libsimilarity_transform.so
+    EIGEN_VALUE_LIB=$L run everyr2_$V 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --every-ab "2;2:0:3;2:0:4;2:0:6;2:4:4;2:8:4;2:16:0" --steps 100 --passes 7 --ab-json $O/r04_everyr2_hilbert8192_f64_$V.json
+    grep median $O/everyr2_$V.log | sed "s/^/$V /"
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
