@@ -24,6 +24,10 @@ if [ "${1:-run}" = build ]; then
     -Wl,-rpath,'$ORIGIN' -o $D/capi_sanitize
   echo "built $D/capi_sanitize"
 else
-  # verify_asan_link_order=0: the environment may preload a library first
-  ASAN_OPTIONS=verify_asan_link_order=0:detect_leaks=1 $D/capi_sanitize
+  # verify_asan_link_order=0: the environment may preload a library first;
+  # leaks inside the HIP / HSA / RCCL runtimes (their process-lifetime
+  # allocations) are not this library's and are suppressed
+  printf 'leak:libamdhip64.so\nleak:libhsa-runtime64.so\nleak:librccl.so\n' > $D/lsan.supp
+  ASAN_OPTIONS=verify_asan_link_order=0:detect_leaks=1 LSAN_OPTIONS=suppressions=$D/lsan.supp \
+    $D/capi_sanitize
 fi
