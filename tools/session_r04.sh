@@ -91,7 +91,7 @@ ragged)
     run ragged_h${N}_p${P} 240 python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --every-ab "0;0" --steps 100 --passes 5 --ab-json $O/r04_ragged_h${N}_p${P}.json
     grep median $O/ragged_h${N}_p${P}.log
   done ;;
-hostasan) run host_asan 300 bash tools/host_asan.sh run; tail -40 $O/host_asan.log | grep -v "^$" | tail -30 ;;
+hostasan) LEAKS=0 run host_asan 120 bash tools/host_asan.sh run; tail -40 $O/host_asan.log | grep -v "^$" | tail -30 ;;
 everyr2)
   # the every-round cached launch (the headline): 1 row (shipped) vs 2 rows
   # per workgroup (probe build), each under workgroup caps and piece tiles
