@@ -28,6 +28,7 @@
 #include <cstring>
 #include <functional>
 #include <memory>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -191,11 +192,20 @@ init_with_deadline(const std::shared_ptr<InitJob>& job,
       const double t_ab = elapsed();
       while (!__atomic_load_n(&job->done, __ATOMIC_ACQUIRE) && elapsed() < t_ab + 10.0)
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
-      ::st::set_error("%s: RCCL rank %d (device %d) still in progress after "
-                      "%.1f s (deadline %.1f s, ST_COMM_TIMEOUT_S / "
-                      "st_set_comm_timeout): a peer did not arrive; %d "
-                      "communicator(s) aborted",
-                      what, ranks[0], devs[0], el, limit, aborted);
+      // name the rank (or, for a single-process group, every rank and
+      // device: any of them may be the one stalled)
+      std::string who = "RCCL rank " + std::to_string(ranks[0]) + " (device " +
+                        std::to_string(devs[0]) + ")";
+      if (job->comms.size() > 1) {
+        who = "RCCL ranks 0.." + std::to_string(job->comms.size() - 1) + " (devices";
+        for (size_t i = 0; i < job->comms.size(); i++)
+          who += " " + std::to_string(devs[i]);
+        who += ")";
+      }
+      ::st::set_error("%s: %s still in progress after %.1f s (deadline %.1f s, "
+                      "ST_COMM_TIMEOUT_S / st_set_comm_timeout): a peer did not "
+                      "arrive; %d communicator(s) aborted",
+                      what, who.c_str(), el, limit, aborted);
       return -1;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(500));
