@@ -4,12 +4,14 @@
 // wider blocks (more bytes); this probe keeps the bytes
 // and changes only the pitch: the every-round flat walk of non-temporal
 // blocks (256-thread workgroups, 2 rows x one 4 KB piece, pieces tiled by 4
-// row groups, non-temporal loads and stores, x * 1.0, one partial per
+// row groups, non-temporal loads and stores, x * f with f = 1.0 passed at
+// run time (a constant 1.0 lets the compiler drop the store), one partial per
 // workgroup and row as k_flat writes) over R x C doubles stored with a row
 // pitch of C + pad doubles.  Median of 7 passes of 8 rounds.
 //
 // Build: make -C tools pitch_probe
-// Run:   ./tools/pitch_probe 8192x65536 16384x32768 32768x32768   (PP_PADS=0,64,512,1024)
+// Run:   ./tools/pitch_probe 8192x65536 16384x32768 32768x32768
+//        (PP_PADS=0,64,512,1024 PP_PT=4 tiles of row groups, PP_RO=1 read only)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -31,7 +33,8 @@
 typedef double d2 __attribute__((ext_vector_type(2)));
 
 __global__ __launch_bounds__(256) void
-k_walk(double* a, double* part, unsigned nrows, unsigned ncols, size_t pitch, unsigned pt)
+k_walk(double* a, double* part, unsigned nrows, unsigned ncols, size_t pitch, unsigned pt,
+       double f, int ro)
 {
   const unsigned ppr = ncols / 512, ng = nrows / 2;
   const unsigned b = blockIdx.x;
@@ -43,7 +46,8 @@ k_walk(double* a, double* part, unsigned nrows, unsigned ncols, size_t pitch, un
   for (int j = 0; j < 2; j++) {
     d2* x = reinterpret_cast<d2*>(a + (size_t)(2 * rg + j) * pitch + (size_t)p * 512) + threadIdx.x;
     const d2 v = __builtin_nontemporal_load(x);
-    __builtin_nontemporal_store(v * 1.0, x);
+    if (!ro) // uniform
+      __builtin_nontemporal_store(v * f, x); // f = 1.0 at run time: the store stays
     s[j] = v.x + v.y;
   }
 #pragma unroll
@@ -78,6 +82,8 @@ int
 main(int argc, char** argv)
 {
   std::vector<unsigned> pads = { 0, 64, 512, 1024 };
+  const int ro = std::getenv("PP_RO") ? std::atoi(std::getenv("PP_RO")) : 0; // read only
+  const unsigned pt = std::getenv("PP_PT") ? (unsigned)std::atoi(std::getenv("PP_PT")) : 4u;
   if (const char* e = std::getenv("PP_PADS")) {
     pads.clear();
     for (const char* q = e; *q;) {
@@ -92,7 +98,7 @@ main(int argc, char** argv)
       std::fprintf(stderr, "bad size %s (RxC, C a multiple of 512, R of 8)\n", argv[i]);
       return 2;
     }
-    const double gb = 2.0 * nr * (double)nc * 8 / 1e9;
+    const double gb = (ro ? 1.0 : 2.0) * nr * (double)nc * 8 / 1e9;
     for (unsigned pad : pads) {
       const size_t pitch = (size_t)nc + pad, n = (size_t)nr * pitch;
       double *a = nullptr, *part = nullptr;
@@ -105,12 +111,12 @@ main(int argc, char** argv)
       HIPCHECK(hipEventCreate(&e0));
       HIPCHECK(hipEventCreate(&e1));
       for (int k = 0; k < 4; k++)
-        hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, 0, a, part, nr, nc, pitch, 4u);
+        hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, 0, a, part, nr, nc, pitch, pt, 1.0, ro);
       std::vector<float> t;
       for (int rep = 0; rep < 7; rep++) {
         HIPCHECK(hipEventRecord(e0));
         for (int k = 0; k < 8; k++)
-          hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, 0, a, part, nr, nc, pitch, 4u);
+          hipLaunchKernelGGL(k_walk, dim3(grid), dim3(256), 0, 0, a, part, nr, nc, pitch, pt, 1.0, ro);
         HIPCHECK(hipEventRecord(e1));
         HIPCHECK(hipEventSynchronize(e1));
         float ms = 0;
@@ -119,8 +125,8 @@ main(int argc, char** argv)
       }
       HIPCHECK(hipGetLastError());
       std::sort(t.begin(), t.end());
-      std::printf("%ux%u fp64, pitch %zu (+%u): %.4f ms per round, %.1f GB/s\n", nr, nc, pitch,
-                  pad, t[3], gb / (t[3] * 1e-3));
+      std::printf("%ux%u fp64 %s tiles %u, pitch %zu (+%u): %.4f ms per round, %.1f GB/s\n", nr,
+                  nc, ro ? "read" : "read+write", pt, pitch, pad, t[3], gb / (t[3] * 1e-3));
       std::fflush(stdout);
       HIPCHECK(hipEventDestroy(e0));
       HIPCHECK(hipEventDestroy(e1));

@@ -100,7 +100,11 @@ everyr2)
     EIGEN_VALUE_LIB=$L run everyr2_$V 300 python3 tools/defer_profile.py --kind hilbert --n 8192 --dtype f64 --every-ab "2;2:0:3;2:0:4;2:0:6;2:4:4;2:8:4;2:16:0" --steps 100 --passes 7 --ab-json $O/r04_everyr2_hilbert8192_f64_$V.json
     grep median $O/everyr2_$V.log | sed "s/^/$V /"
   done ;;
-pitch) run pitch_probe 300 ./tools/pitch_probe 8192x65536 16384x32768 32768x32768 4096x131072; cat $O/pitch_probe.log ;;
+pitch)
+  for PT in 4 8; do for RO in 0 1; do
+    PP_PT=$PT PP_RO=$RO PP_PADS=0,32,64,128,512 run pitch_probe_t${PT}_ro${RO} 300 ./tools/pitch_probe 8192x65536 16384x32768 32768x32768 8192x8192
+    cat $O/pitch_probe_t${PT}_ro${RO}.log
+  done; done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
