@@ -105,6 +105,15 @@ pitch)
     PP_PT=$PT PP_RO=$RO PP_PADS=0,32,64,128,512 run pitch_probe_t${PT}_ro${RO} 300 ./tools/pitch_probe 8192x65536 16384x32768 32768x32768 8192x8192
     cat $O/pitch_probe_t${PT}_ro${RO}.log
   done; done ;;
+nttile)
+  # the every-round non-temporal launch's piece tile (st_set_every_tile via
+  # --every-ab "0:T"): shipped 4 against 8 / 16 / row-major, on the north
+  # star, configs[4] and the configs[3] rank blocks
+  for W in "32768 0 f64" "65536 8 f64" "65536 4 f64" "32768 0 f32"; do
+    set -- $W; N=$1; P=$2; DT=$3
+    run nttile_r${N}_p${P}_${DT} 300 python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype $DT --every-ab "0;0:8;0:16;0:1;0:4" --steps 20 --passes 5 --ab-json $O/r04_nttile_r${N}_p${P}_${DT}.json
+    grep median $O/nttile_r${N}_p${P}_${DT}.log
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
