@@ -251,6 +251,12 @@ ld(const V* p)
 #ifndef ST_PROBE_FORMS
 #define ST_PROBE_FORMS 0
 #endif
+// (probe builds only) k_flat's row pitch = ncols + ST_PITCH_PAD elements:
+// the matrix walk at the same bytes with a padded pitch (tools/flat_map_sweep)
+#ifndef ST_PITCH_PAD
+#define ST_PITCH_PAD 0
+#endif
+static_assert(ST_PROBE_FORMS || ST_PITCH_PAD == 0, "ST_PITCH_PAD: probe builds only");
 
 #ifndef ST_ROW_VLOAD
 #define ST_ROW_VLOAD 0
@@ -1119,7 +1125,8 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     cl[u] = (!UM || in_cols[u]) ? c0 + u * BLK * W : ncols - W;
   // the group's rows walked from one base pointer by the row pitch (no
   // per-row 64-bit multiply); rows past the block re-read its last row
-  const T* ap = a + (size_t)(r0 < nrows ? r0 : nrows - 1) * ncols;
+  const size_t lda = (size_t)ncols + ST_PITCH_PAD; // row pitch
+  const T* ap = a + (size_t)(r0 < nrows ? r0 : nrows - 1) * lda;
 #pragma unroll
   for (int j = 0; j < R; j++) {
     acc[j] = (T)0;
@@ -1128,12 +1135,12 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
       for (int u = 0; u < U; u++)
         x[u][j] = ld<V, NTL>(reinterpret_cast<const V*>(ap + cl[u]));
       if (r0 + j + 1 < nrows) // uniform
-        ap += ncols;
+        ap += lda;
     } else {
 #pragma unroll
       for (int u = 0; u < U; u++)
         if (in[u] && r0 + j < nrows)
-          x[u][j] = ld<V, NTL>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 +
+          x[u][j] = ld<V, NTL>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * lda + c0 +
                                                    u * BLK * W));
     }
   }
@@ -1248,7 +1255,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         }
       }
     }
-    T* wp = a + (size_t)r0 * ncols + c0 + u * BLK * W; // row r0 + j after j pitches
+    T* wp = a + (size_t)r0 * lda + c0 + u * BLK * W; // row r0 + j after j pitches
 #pragma unroll
     for (int j = 0; j < R; j++) {
       const T inv = NP >= 0 ? sr[j] : (T)1 / sr[j];
@@ -1259,7 +1266,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         y = (inv * x[u][j]) * sc[u]; // main.py:13-16
       if (do_store && in_cols[u] && r0 + j < nrows)
         st<V, NTS>(reinterpret_cast<V*>(wp), y);
-      wp += ncols;
+      wp += lda;
       const T h = in_cols[u] ? hsum<T, W>(y) : (T)0;
       acc[j] = u == 0 ? h : acc[j] + h;
     }
@@ -1305,7 +1312,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
         else
           y = (inv * x[u][j]) * sc[u]; // main.py:13-16
         if (do_store)
-          st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * ncols + c0 + u * BLK * W),
+          st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * lda + c0 + u * BLK * W),
                     y);
         acc[j] = u == 0 ? hsum<T, W>(y) : acc[j] + hsum<T, W>(y);
       }

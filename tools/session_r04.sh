@@ -114,6 +114,13 @@ nttile)
     run nttile_r${N}_p${P}_${DT} 300 python3 tools/defer_profile.py --kind random --n $N --rank-block $P --dtype $DT --every-ab "0;0:8;0:16;0:1;0:4" --steps 20 --passes 5 --ab-json $O/r04_nttile_r${N}_p${P}_${DT}.json
     grep median $O/nttile_r${N}_p${P}_${DT}.log
   done ;;
+pitchflat)
+  # k_flat's own every-round walk (tiles of 4 row groups, as shipped) with the
+  # row pitch padded by 0 / 32 / 64 doubles at the same bytes
+  for V in flat_map_sweep flat_map_sweep_pad32 flat_map_sweep_pad64; do
+    FMS_EVERY=1 FMS_PT=4 run pitchflat_$V 300 ./tools/$V f64 32768 8192x65536 16384x32768 16384x65536
+    grep -v "^$" $O/pitchflat_$V.log | sed "s/^/$V /"
+  done ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
