@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
@@ -58,13 +59,14 @@ namespace {
 // the call returns -1 with the stalled rank and device named, instead of
 // hanging in ncclCommInitRank / ncclCommInitAll / the first all-gather.
 // ---------------------------------------------------------------------------
-double g_comm_timeout_s = -1.0; // < 0: ST_COMM_TIMEOUT_S or 120 s
+std::atomic<double> g_comm_timeout_s{ -1.0 }; // < 0: ST_COMM_TIMEOUT_S or 120 s
 
 double
 comm_timeout_s()
 {
-  if (g_comm_timeout_s >= 0.0)
-    return g_comm_timeout_s;
+  const double set = g_comm_timeout_s.load(std::memory_order_relaxed);
+  if (set >= 0.0)
+    return set;
   const char* e = std::getenv("ST_COMM_TIMEOUT_S");
   const double v = e ? std::atof(e) : 0.0;
   return v > 0.0 ? v : 120.0;
@@ -649,7 +651,7 @@ double
 st_set_comm_timeout(double seconds)
 {
   const double old = st::comm_timeout_s();
-  st::g_comm_timeout_s = seconds > 0.0 ? seconds : -1.0;
+  st::g_comm_timeout_s.store(seconds > 0.0 ? seconds : -1.0, std::memory_order_relaxed);
   return old;
 }
 
