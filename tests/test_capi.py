@@ -295,3 +295,45 @@ def test_launch_policy_rejects_bad_queries():
     assert L.st_launch_policy_query(1, 8192, 8192, 1, 5, ctypes.byref(out)) < 0   # 5 w/o store
     assert L.st_launch_policy_query(1, 8192, 8192, 2, 5, ctypes.byref(out)) == 0
     assert out.rows == 8 and out.tile == 16 and out.store_nt == 0
+
+
+def test_launch_policy_matches_the_hardware_traces():
+    """The pinned map against what actually ran on the GPU: every k_flat and
+    k_mfree instantiation in the committed rocprof kernel statistics of the
+    headline workloads (profiles/r04_*_kernel_stats.csv, `bench.py --kind K
+    --n N --dtype D`) has the rows per workgroup, piece bytes and load /
+    store cache policy st_launch_policy_query gives for its form (the
+    every-round round, a deferred read-only round, a storing round or a
+    flush with NP pending, the matrix-free round)."""
+    import csv
+    import re
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cases = (("r04_hilbert8192_f64_kernel_stats.csv", "f64", 8192),
+             ("r04_random32768_f64_kernel_stats.csv", "f64", 32768),
+             ("r04_random32768_f32_kernel_stats.csv", "f32", 32768))
+    checked = 0
+    for fname, dt, n in cases:
+        size = 8 if dt == "f64" else 4
+        for row in csv.DictReader(open(os.path.join(root, "profiles", fname))):
+            name = row["Name"]
+            m = re.search(r"k_flat<([^>]*)>", name)
+            if m:
+                a = [x.strip() for x in m.group(1).split(",")]
+                W, NT, R, BLK, NP, U, DS, FL = (int(a[1]), a[3] == "true", int(a[4]),
+                                                int(a[8]), int(a[11]), int(a[12]),
+                                                int(a[14]), int(a[16]))
+                form = (_lib.ST_FORM_ROUND if NP < 0 else
+                        _lib.ST_FORM_DEFER_STORE if DS == 1 else _lib.ST_FORM_DEFER_READ)
+                p = _lib.launch_policy(dt, n, n, form, max(NP, 0))
+                assert p["rows"] == R and p["piece_bytes"] == BLK * W * U * size, (fname, a)
+                assert p["load_nt"] == int(NT != bool(FL & 1)), (fname, a)
+                if form != _lib.ST_FORM_DEFER_READ:
+                    assert p["store_nt"] == int(NT != bool(FL & 2)), (fname, a)
+                checked += 1
+            m = re.search(r"k_mfree<([^>]*)>", name)
+            if m:
+                a = [x.strip() for x in m.group(1).split(",")]
+                p = _lib.launch_policy(dt, n, n, _lib.ST_FORM_MFREE)
+                assert p["rows"] == int(a[1]) and p["load_nt"] == int(a[4] == "true"), (fname, a)
+                checked += 1
+    assert checked >= 20
