@@ -1,0 +1,104 @@
+#!/usr/bin/env python3
+"""Extended parity sweep on the GPU against the CPU oracle (the test suite's
+test_fuzz_vs_oracle, widened): seeded random cases over size (including the
+flat round's deferred-write sizes from 144 MiB and ragged, odd and
+non-16-byte widths), dtype, semantics, form (transform with deferred writes,
+transform storing every round, matrix-free), batch, eps and input kind,
+through the drop-in host path and the device-resident solver.  Every case
+must reproduce the oracle's iteration count; λ and v are held to the test
+suite's tolerances (fp64 1e-10, fp32 2e-5 / 5e-4) and the worst errors are
+recorded.  Test infrastructure: the oracle is the checker.
+
+    python3 tools/fuzz_parity.py --cases 300 --json OUT.json
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, HERE)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--cases", type=int, default=300)
+    p.add_argument("--seed", type=int, default=20261017)
+    p.add_argument("--json", default=None)
+    a = p.parse_args()
+    import numpy as np
+    import torch
+    from eigen_value_amd import device as dev
+    from eigen_value_amd.similarity_transform import EigenValue
+    from oracle import oracle as orc
+    torch.cuda.set_device(0)
+    rng = np.random.default_rng(a.seed)
+    small = [1, 2, 3, 5, 7, 16, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 1000, 1023,
+             1024, 1025, 2047, 2049, 2051, 3001]
+    flat = [4352, 4353, 4480, 5000, 5121, 6144]           # >= 144 MiB fp64: the flat round
+    worst = {"f64": {"lam": 0.0, "v": 0.0}, "f32": {"lam": 0.0, "v": 0.0}}
+    out = {"seed": a.seed, "cases": [], "skipped_fp32_borderline": 0}
+    solver = dev.DeviceSolver("cuda:0")
+    t0 = time.time()
+    with EigenValue() as ev:
+        for case in range(a.cases):
+            big = rng.random() < 0.25
+            n = int(rng.choice(flat if big else small))
+            dt = np.float64 if (big or rng.random() < 0.6) else np.float32
+            sem = int(rng.integers(0, 2))
+            form = str(rng.choice(["deferred", "every", "mfree"]))
+            batch = int(rng.choice([0, 1, 2, 5, 8]))
+            eps = float(rng.choice([1e-3, 1e-6, 1e-2]))
+            kind = "hilbert" if rng.random() < 0.5 else "random"
+            path = "device" if rng.random() < 0.5 else "dropin"
+            max_itr = 60 if big else 200
+            mat = orc.hilbert(n, dt) if kind == "hilbert" else orc.random_matrix(n, case, dt)
+            if path == "dropin":
+                lam, v, _, itr, _ = ev.similarity_transform_ex(
+                    mat, eps=eps, semantics=sem, matrix_free=form == "mfree", batch=batch,
+                    max_itr=max_itr, write_every_round=form == "every")
+            else:
+                t = torch.from_numpy(mat).to("cuda:0")
+                lam, v, itr, _ = solver.solve(t, eps=eps, semantics=sem,
+                                              matrix_free=form == "mfree", batch=batch,
+                                              max_itr=max_itr,
+                                              write_every_round=form == "every")
+                v = v.cpu().numpy()
+                del t
+            ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=max_itr,
+                                           nthreads=16)
+            key = "f64" if dt == np.float64 else "f32"
+            dmin = np.min(np.abs(ref.max_dsum - eps)) if len(ref.max_dsum) else 1.0
+            if key == "f32" and dmin < 1e-5 * max(1.0, float(np.max(mat.sum(1)))):
+                out["skipped_fp32_borderline"] += 1
+                continue
+            el = abs(float(lam) - float(ref.eigen_val)) / max(abs(float(ref.eigen_val)), 1e-300)
+            evv = float(np.max(np.abs(np.asarray(v, dtype=np.float64) - ref.eigen_vec)))
+            tol_l, tol_v = (1e-10, 1e-10) if key == "f64" else (2e-5, 5e-4)
+            ok = itr == ref.iter_count and el <= tol_l and evv <= tol_v
+            worst[key]["lam"] = max(worst[key]["lam"], el)
+            worst[key]["v"] = max(worst[key]["v"], evv)
+            rec = {"case": case, "n": n, "dtype": key, "sem": sem, "form": form, "batch": batch,
+                   "eps": eps, "kind": kind, "path": path, "iters": int(itr),
+                   "iters_oracle": int(ref.iter_count), "lam_rel_err": el, "v_max_err": evv,
+                   "ok": bool(ok)}
+            out["cases"].append(rec)
+            print(json.dumps(rec), flush=True)
+            if not ok:
+                print(f"MISMATCH {rec}", flush=True)
+    solver.close()
+    out["worst"] = worst
+    out["n_cases"] = len(out["cases"])
+    out["n_ok"] = sum(c["ok"] for c in out["cases"])
+    out["seconds"] = round(time.time() - t0, 1)
+    print(f"{out['n_ok']} / {out['n_cases']} cases match the oracle "
+          f"({out['skipped_fp32_borderline']} fp32 borderline stops skipped); worst {worst}",
+          flush=True)
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=0)
+    return 0 if out["n_ok"] == out["n_cases"] else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -121,6 +121,7 @@ pitchflat)
     FMS_EVERY=1 FMS_PT=4 run pitchflat_$V 300 ./tools/$V f64 32768 8192x65536 16384x32768 16384x65536
     grep -v "^$" $O/pitchflat_$V.log | sed "s/^/$V /"
   done ;;
+fuzz) run fuzz_parity 900 python3 -u tools/fuzz_parity.py --cases 300 --json $O/r04_fuzz_parity.json; tail -3 $O/fuzz_parity.log ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
