@@ -931,7 +931,7 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
   // fp64: cached, non-temporal (the cached storing round uncapped since
   // round 4: caps 0 / 3 / 4 tie within 0.1 % on 8192^2 and the three
   // weak-scaled rank blocks once it is tiled by 16, 2 loses 1-2 %,
-  // profiles/r04_storeab_*_s5t16.json)
+  // profiles/r04_storeab.json, runs *_s5t16)
   { { 0, 4, 4, 3, 3, 0, 0 }, { 0, 5, 4, 4, 4, 0, 3 } },
 };
 
@@ -1060,7 +1060,7 @@ defer_tile(int np, bool store)
   constexpr bool kF64C = !NT && sizeof(T) == 8;
   // storing rounds row-major, but the cached fp64 one with 5 pending (on
   // non-temporal blocks tiles of 4 ... 32 lose 0.3 - 6 %,
-  // profiles/r04_ntstore_*.json)
+  // profiles/r04_ntstore.json)
   if (store)
     return (np >= 5 && kF64C && ST_DEFER_STORE_R8_CACHED) ? (uint32_t)ST_DEFER_TS5_CACHED
                                                            : 0u;
