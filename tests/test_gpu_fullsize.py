@@ -317,3 +317,36 @@ def test_comm_init_deadline_names_the_stalled_rank(tmp_path):
     assert int(rc) < 0 and null == "True"
     assert 3.0 <= float(el) < 60.0
     assert "still in progress" in lines["ERR"] and "rank 0 (device 0)" in lines["ERR"]
+
+
+_DUPLICATE_PROBE = r"""
+import sys, time
+sys.path.insert(0, sys.argv[1])
+from eigen_value_amd import _lib
+from eigen_value_amd.multi import solve_multi
+_lib.load().st_set_comm_timeout(20.0)
+t0 = time.time()
+try:
+    solve_multi(3001, "random", devices=[0, 0], seed=3)
+    print("RESULT ok")
+except _lib.EigenValueError as e:
+    print("RESULT error", round(time.time() - t0, 2), str(e).replace("\n", " "))
+"""
+
+
+def test_native_multi_gpu_grouped_init_failure_is_prompt(tmp_path):
+    """st_solve_multi_* over two ranks on one device (RCCL refuses a device
+    twice): the grouped non-blocking init on the helper thread reports the
+    failure as an error naming the call, promptly, instead of hanging - the
+    multi-device init path's failure handling, exercised on a one-GPU box.
+    (If a future RCCL accepts it, the solve simply has to succeed.)"""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _DUPLICATE_PROBE, repo], capture_output=True,
+                         text=True, timeout=150)
+    assert out.returncode == 0, out.stderr[-3000:]
+    line = [ln for ln in out.stdout.splitlines() if ln.startswith("RESULT")][-1]
+    if line.startswith("RESULT error"):
+        el = float(line.split()[2])
+        assert el < 60 and "st_solve_multi" in line, line
