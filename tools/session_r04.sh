@@ -122,6 +122,7 @@ pitchflat)
     grep -v "^$" $O/pitchflat_$V.log | sed "s/^/$V /"
   done ;;
 fuzz) run fuzz_parity 900 python3 -u tools/fuzz_parity.py --cases 300 --json $O/r04_fuzz_parity.json; tail -3 $O/fuzz_parity.log ;;
+commtests) run comm_tests 300 python -u -m pytest tests/test_gpu_fullsize.py -k "prompt or deadline" -v --timeout 200 --timeout-method thread; tail -6 $O/comm_tests.log ;;
 tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q -rs --timeout 300 --timeout-method thread ;;
 bench) run bench 600 python bench.py ;;
 prof)
