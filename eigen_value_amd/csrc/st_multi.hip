@@ -136,7 +136,12 @@ comm_wait(const ncclComm_t* comms, int n, const int* ranks, const int* devs,
 // thread-local to the thread that ended the group: the helper must not
 // exit before the communicators are ready), and this thread waits for it at
 // most the deadline; past it, every handle RCCL wrote is aborted and the
-// helper is given a few seconds to return.
+// helper is given a few seconds to return.  RCCL's abort does not always
+// unblock it (tests/test_gpu_fullsize.py: returned at once in some runs,
+// not within 10 s in another), and a process that then exits normally can
+// crash in the runtimes' teardown behind the blocked thread, so the error
+// says so: a job that lost a peer should end with _exit (bench.py's
+// watchdog does).
 struct InitJob
 {
   std::vector<ncclComm_t> comms; // written by RCCL (early)
@@ -204,10 +209,14 @@ init_with_deadline(const std::shared_ptr<InitJob>& job,
           who += " " + std::to_string(devs[i]);
         who += ")";
       }
+      const bool stuck = !__atomic_load_n(&job->done, __ATOMIC_ACQUIRE);
       ::st::set_error("%s: %s still in progress after %.1f s (deadline %.1f s, "
                       "ST_COMM_TIMEOUT_S / st_set_comm_timeout): a peer did not "
-                      "arrive; %d communicator(s) aborted",
-                      what, who.c_str(), el, limit, aborted);
+                      "arrive; %d communicator(s) aborted%s",
+                      what, who.c_str(), el, limit, aborted,
+                      stuck ? "; the RCCL init thread did not return and is left "
+                              "behind (end the process with _exit)"
+                            : "");
       return -1;
     }
     std::this_thread::sleep_for(std::chrono::microseconds(500));

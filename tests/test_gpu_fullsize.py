@@ -296,7 +296,12 @@ comm = ctypes.c_void_p()
 t0 = time.time()
 rc = L.st_comm_init(ctypes.byref(comm), 2, 0, uid.raw, 0)   # rank 1 never joins
 print("RC", rc, "EL", round(time.time() - t0, 2), "NULL", comm.value is None)
-print("ERR", _lib.last_error())
+print("ERR", _lib.last_error(), flush=True)
+# a job that lost a peer ends; with _exit, as bench.py's watchdog does: a
+# normal exit can crash in the runtimes' teardown behind an init thread
+# RCCL's abort did not unblock (the error message says whether it did)
+import os
+os._exit(0)
 """
 
 
@@ -315,7 +320,7 @@ def test_comm_init_deadline_names_the_stalled_rank(tmp_path):
     lines = dict(ln.split(" ", 1) for ln in out.stdout.splitlines() if ln[:3] in ("RC ", "ERR"))
     rc, _, el, _, null = lines["RC"].split()
     assert int(rc) < 0 and null == "True"
-    assert 3.0 <= float(el) < 60.0
+    assert 3.0 <= float(el) < 30.0        # the deadline + at most 10 s for the helper
     assert "still in progress" in lines["ERR"] and "rank 0 (device 0)" in lines["ERR"]
 
 
