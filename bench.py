@@ -1284,6 +1284,12 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+        if sharded.INIT_THREAD_LEFT_BEHIND:
+            # a library communicator's init thread is still blocked (RCCL's
+            # abort did not release it): end without the runtimes' teardown
+            sys.stdout.flush()
+            sys.stderr.flush()
+            os._exit(0)
 
 
 if __name__ == "__main__":

@@ -219,6 +219,12 @@ class RcclComm:
             self.comm = self.ctypes.c_void_p()
 
 
+# set when st_comm_init reported that RCCL's abort left its init thread
+# blocked (st_multi.hip init_with_deadline): the process should end with
+# os._exit, since a normal exit can crash in the runtimes' teardown behind it
+INIT_THREAD_LEFT_BEHIND = False
+
+
 def make_comm_agreed(group, factory, device=None):
     """factory() on every rank of `group`, then one all-reduce (MIN) of
     whether it succeeded: a communicator is used only if EVERY rank has one
@@ -231,11 +237,14 @@ def make_comm_agreed(group, factory, device=None):
     which their st_comm_init aborts and returns an error too."""
     import torch
     import torch.distributed as dist
+    global INIT_THREAD_LEFT_BEHIND
     comm, err = None, None
     try:
         comm = factory()
     except Exception as e:  # noqa: BLE001 - agreed on below
         err = f"{type(e).__name__}: {e}"
+        if "left behind" in err:
+            INIT_THREAD_LEFT_BEHIND = True
     flag = torch.tensor([0 if comm is None else 1], dtype=torch.int32,
                         device=device if device is not None else "cpu")
     dist.all_reduce(flag, op=dist.ReduceOp.MIN, group=group)
