@@ -557,13 +557,19 @@ def _agree_worker(rank, world, port, fail_rank, outdir):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        import eigen_value_amd.sharded as shd
+
         def factory():
             if rank == fail_rank:
-                raise RuntimeError("no RCCL here")
+                # as st_comm_init reports a deadline whose abort did not
+                # release RCCL's init thread
+                raise RuntimeError("still in progress ...; the RCCL init thread did not "
+                                   "return and is left behind (end the process with _exit)")
             return _FakeComm()
         comm, err = make_comm_agreed(None, factory)
         np.save(os.path.join(outdir, f"agree{rank}.npy"),
-                np.array([comm is not None, _FakeComm.closed, err is not None]))
+                np.array([comm is not None, _FakeComm.closed, err is not None,
+                          shd.INIT_THREAD_LEFT_BEHIND]))
     finally:
         dist.destroy_process_group()
 
@@ -578,9 +584,11 @@ def test_library_comm_is_used_only_if_every_rank_has_one(tmp_path, fail_rank):
     mp.spawn(_agree_worker, args=(4, _free_port(), fail_rank, str(tmp_path)), nprocs=4,
              join=True)
     for r in range(4):
-        has, closed, err = np.load(tmp_path / f"agree{r}.npy")
+        has, closed, err, left = np.load(tmp_path / f"agree{r}.npy")
         if fail_rank < 0:
             assert has and not closed and not err
         else:
             assert not has and err
             assert closed == (0 if r == fail_rank else 1)    # the others closed theirs
+        # the failing rank knows to end with _exit (bench.py does)
+        assert bool(left) == (r == fail_rank)
