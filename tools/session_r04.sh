@@ -117,7 +117,7 @@ nttile)
 pitchflat)
   # k_flat's own every-round walk (tiles of 4 row groups, as shipped) with the
   # row pitch padded by 0 / 32 / 64 doubles at the same bytes
-  for V in flat_map_sweep flat_map_sweep_pad32 flat_map_sweep_pad64; do
+  for V in ${PITCH_VARIANTS:-flat_map_sweep flat_map_sweep_pad32 flat_map_sweep_pad64}; do
     FMS_EVERY=1 FMS_PT=4 run pitchflat_$V 300 ./tools/$V f64 32768 8192x65536 16384x32768 16384x65536
     grep -v "^$" $O/pitchflat_$V.log | sed "s/^/$V /"
   done ;;
