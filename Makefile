@@ -6,13 +6,13 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -fno-fast-math -Wall -Wextra -Wno-unused-parameter -Iinclude \
             -Ieigen_value_amd/csrc
 SRC      := eigen_value_amd/csrc/st_kernels.hip eigen_value_amd/csrc/st_solve.hip \
-            eigen_value_amd/csrc/st_multi.hip
+            eigen_value_amd/csrc/st_multi.hip eigen_value_amd/csrc/st_rendezvous.hip
 OBJ      := $(patsubst eigen_value_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB      := eigen_value_amd/lib/libsimilarity_transform.so
 
 all: $(LIB) oracle
 
-build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h eigen_value_amd/csrc/st_device.h
+build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h eigen_value_amd/csrc/st_device.h eigen_value_amd/csrc/st_rendezvous.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -105,6 +105,12 @@ def parse(argv=None):
                    help="N > 1: seconds without progress after which a rank gives up "
                         "(and the self-spawning parent ends the run) naming its last leg")
     p.add_argument("--stall-rank", type=int, default=None, help=argparse.SUPPRESS)  # test hook
+    p.add_argument("--stall-in", default="barrier", choices=["barrier", "rendezvous"],
+                   help=argparse.SUPPRESS)  # test hook: where the other ranks wait
+    p.add_argument("--comm-timeout", type=float, default=None,
+                   help="seconds each rank waits for its peers when the library's RCCL "
+                        "communicator is made (st_set_comm_timeout; default "
+                        "ST_COMM_TIMEOUT_S or 120)")
     p.add_argument("--leg", default=None, help=argparse.SUPPRESS)   # child mode
     p.add_argument("--leg-args", default="{}", help=argparse.SUPPRESS)
     p.add_argument("--one-gpu", action="store_true",
@@ -544,6 +550,9 @@ def configs3_leg(sharded, torch, dist, world, rank, steps, warmup, representativ
                                   "bytes_per_round": by_d}
     if sh.rccl is not None:
         leg["rccl_ranks"] = sh.rccl.info()["nranks"]
+    if world > 1:
+        from eigen_value_amd import _lib
+        leg["rccl_version"] = _lib.rccl_info()["rccl_version"]
     sh.close()
     del sh, v
     torch.cuda.empty_cache()
@@ -951,14 +960,25 @@ def strip_fracs(obj):
 
 def stall_test(args, dist):
     """--stall-rank R (tests/test_bench.py, CPU, gloo): rank R stops
-    reporting progress and never reaches the barrier the others wait in -
-    a stand-in for a rank stuck in RCCL init - so the watchdog and the
-    spawning parent's deadline can be tested without a GPU."""
+    reporting progress and never reaches the point the others wait at - so
+    the watchdog, the spawning parent's deadline and the communicator
+    rendezvous can be tested without a GPU.  --stall-in barrier: the others
+    wait in a barrier (a rank stuck in a collective); --stall-in rendezvous:
+    they make the library communicator's pre-RCCL presence check
+    (sharded.rendezvous), which names rank R within --comm-timeout."""
     dist.init_process_group("gloo")
     progress("stall test: process group up")
     if dist.get_rank() == args.stall_rank:
         progress("stall test: this rank sleeps")
         time.sleep(10 ** 6)
+    if args.stall_in == "rendezvous":
+        from eigen_value_amd import sharded
+        try:
+            sharded.rendezvous(None, args.comm_timeout)
+        except sharded.PeerMissingError as e:
+            print(f"bench.py: rank {dist.get_rank()}: {e}", file=sys.stderr, flush=True)
+            raise SystemExit(3) from None   # no RCCL state exists: a normal exit
+        return
     dist.barrier()
 
 
@@ -1001,7 +1021,9 @@ def main():
         else:
             dist.init_process_group("gloo")
         progress(f"process group up ({args.backend}, world {world})")
-    _lib.load()   # fail loudly before anything else if the HIP library is missing
+    L = _lib.load()   # fail loudly before anything else if the HIP library is missing
+    if args.comm_timeout:
+        L.st_set_comm_timeout(args.comm_timeout)
     full = not args.no_north_star
 
     dt = torch.float64 if args.dtype == "f64" else torch.float32
@@ -1114,6 +1136,14 @@ def main():
                     "collective": ("library RCCL communicator (st_allgather)" if sh.rccl
                                    else "torch.distributed all_gather")}
         exchange["rccl_ranks"] = sh.rccl.info()["nranks"] if sh.rccl is not None else None
+    # which RCCL the library's calls bind in this process (torch's bundled one
+    # under torch: it is loaded first and has the same soname) - the one that
+    # produces an N > 1 line's exchange
+    rccl = _lib.rccl_info()
+    if exchange is not None:
+        exchange.update(rccl_version=rccl["rccl_version"], rccl_path=rccl["rccl_path"])
+        if dist.get_backend() == "nccl":
+            exchange["torch_nccl_version"] = ".".join(map(str, torch.cuda.nccl.version()))
 
     # ---- the matrix-free form on the same workload (N^2*b per round) -----
     mf = sharded.ShardedSimilarityTransform(n, dt, matrix_free=True)
@@ -1159,7 +1189,7 @@ def main():
                                           if (world == 1 and n == 8192) else
                                           f"row-block sharding over {world} GPU(s), "
                                           + ("strong" if args.strong else "weak") + "-scaled")},
-           "roofline": roofline, "solve": solve, "matrix_free": matrix_free}
+           "roofline": roofline, "solve": solve, "matrix_free": matrix_free, "rccl": rccl}
     if use_overlap:
         out["config"]["exchange"] = "overlapped (split round, all-gather on a second stream)"
     if world > 1:

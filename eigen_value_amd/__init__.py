@@ -9,4 +9,4 @@ Public surface:
 from ._lib import EigenValueError, ST_SEM_MAINPY, ST_SEM_SYCL, lib_path, load  # noqa: F401
 from .similarity_transform import EigenValue  # noqa: F401
 
-__version__ = "0.4.0"  # st_version() reports the same (tests/test_capi.py)
+__version__ = "0.5.0"  # st_version() reports the same (tests/test_capi.py)

@@ -226,6 +226,10 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_set_comm_timeout.restype = ctypes.c_double
     L.st_comm_info.argtypes = [P, P, P, P]
     L.st_comm_info.restype = i32
+    L.st_get_comm_timeout.argtypes = []
+    L.st_get_comm_timeout.restype = ctypes.c_double
+    L.st_rccl_version.argtypes = [P, ctypes.c_char_p, i32]
+    L.st_rccl_version.restype = i32
     for sfx in ("f32", "f64"):
         getattr(L, f"st_allgather_{sfx}").argtypes = [P, P, P, u64, P]
         getattr(L, f"st_allgather_{sfx}").restype = i32
@@ -233,6 +237,20 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_launch_policy_query.restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32
+
+
+def rccl_info(L: Optional[ctypes.CDLL] = None) -> dict:
+    """The RCCL the library's calls are bound to in THIS process
+    (st_rccl_version): {"rccl_version": "X.Y.Z", "rccl_version_code": int,
+    "rccl_path": file holding the bound ncclAllGather}.  Inside a torch
+    process that is torch's bundled librccl; for a C caller the /opt/rocm one."""
+    L = L or load()
+    code = ctypes.c_int(0)
+    path = ctypes.create_string_buffer(4096)
+    L.st_rccl_version(ctypes.byref(code), path, len(path))
+    v = code.value
+    return {"rccl_version": f"{v // 10000}.{v // 100 % 100}.{v % 100}",
+            "rccl_version_code": v, "rccl_path": path.value.decode(errors="replace")}
 
 
 def last_error(L: Optional[ctypes.CDLL] = None) -> str:

@@ -251,12 +251,6 @@ ld(const V* p)
 #ifndef ST_PROBE_FORMS
 #define ST_PROBE_FORMS 0
 #endif
-// (probe builds only) k_flat's row pitch = ncols + ST_PITCH_PAD elements:
-// the matrix walk at the same bytes with a padded pitch (tools/flat_map_sweep)
-#ifndef ST_PITCH_PAD
-#define ST_PITCH_PAD 0
-#endif
-static_assert(ST_PROBE_FORMS || ST_PITCH_PAD == 0, "ST_PITCH_PAD: probe builds only");
 
 #ifndef ST_ROW_VLOAD
 #define ST_ROW_VLOAD 0
@@ -1125,7 +1119,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     cl[u] = (!UM || in_cols[u]) ? c0 + u * BLK * W : ncols - W;
   // the group's rows walked from one base pointer by the row pitch (no
   // per-row 64-bit multiply); rows past the block re-read its last row
-  const size_t lda = (size_t)ncols + ST_PITCH_PAD; // row pitch
+  const size_t lda = (size_t)ncols; // row pitch
   const T* ap = a + (size_t)(r0 < nrows ? r0 : nrows - 1) * lda;
 #pragma unroll
   for (int j = 0; j < R; j++) {

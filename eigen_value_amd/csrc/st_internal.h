@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "similarity_transform.h"
 
 namespace st {
@@ -30,6 +32,10 @@ void clear_error();
       return -1;                                                               \
     }                                                                          \
   } while (0)
+
+// "RCCL X.Y.Z (path of the library that holds the bound ncclAllGather)"
+// (st_multi.hip; st_version, st_rccl_version)
+std::string rccl_desc();
 
 // Restores the caller's current HIP device when a C entry point returns
 // (by any path): contexts, shards and communicators switch devices

@@ -1,0 +1,496 @@
+// st_rendezvous.hip — the presence check that st_comm_init runs BEFORE any
+// rank enters RCCL (host code only; no kernels).
+//
+// Why: RCCL's ncclCommInitRankConfig does not return while a peer is missing
+// (blocking = 0 or not), ncclCommAbort from another thread does not reliably
+// release it, and a process that then exits with that thread still inside
+// RCCL crashes in the runtimes' teardown (profiles/r04_comm_deadline_probe.log,
+// VERDICT r04 #3).  So a missing peer must be found before RCCL is entered.
+//
+// How: st_comm_unique_id no longer hands out an RCCL id.  It opens a TCP
+// listener and returns a 128-byte rendezvous id (magic, nonce, IPv4 address
+// and port, host name).  st_comm_init on every rank joins it:
+//   * the process that made the id (the first of its st_comm_init calls to
+//     claim the listener) is the host: it accepts one hello per other rank
+//     (nonce, nranks, rank, device, pid, host) until all nranks are present
+//     or the deadline (st_set_comm_timeout) passes;
+//   * every other rank connects (retrying while the host is not listening
+//     yet), sends its hello and waits for the host's reply;
+//   * all present: the host makes the RCCL unique id (ncclGetUniqueId) and
+//     sends it in the reply; every rank then enters ncclCommInitRankConfig
+//     knowing that every peer is alive and about to do the same;
+//   * otherwise the host's reply names the ranks that did not arrive, every
+//     present rank returns -1 with that message, and no RCCL state exists.
+// The loop being sharded is similarity_transform.cpp:39-53; its per-round
+// host sync (:45-50) is what the all-gather over this communicator replaces.
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <ifaddrs.h>
+#include <net/if.h>
+#include <netinet/in.h>
+#include <netinet/tcp.h>
+#include <poll.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <random>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "st_internal.h"
+#include "st_rendezvous.h"
+
+namespace st {
+namespace {
+
+constexpr char kMagic[8] = { 's', 't', '-', 'r', 'd', 'v', '1', 0 };
+
+struct RdvId // the bytes of st_comm_unique_id's id (kRdvIdBytes)
+{
+  char magic[8];
+  uint64_t nonce;
+  uint32_t addr; // IPv4, network order
+  uint16_t port; // network order
+  uint16_t reserved;
+  char host[64]; // the id maker's host name (messages only)
+};
+static_assert(sizeof(RdvId) <= kRdvIdBytes, "rendezvous id too large");
+
+struct Hello
+{
+  uint64_t nonce;
+  int32_t nranks, rank, device, pid;
+  char host[64];
+};
+
+struct Reply
+{
+  uint64_t nonce;
+  int32_t status; // 0: payload valid; else msg says why
+  int32_t reserved;
+  char payload[kRdvPayloadBytes];
+  char msg[512];
+};
+
+// listeners made by st_comm_unique_id in this process, by nonce; the first
+// st_comm_init that joins an id found here is its host
+std::mutex g_mu;
+std::unordered_map<uint64_t, int> g_listeners;
+
+using Clock = std::chrono::steady_clock;
+
+double
+seconds_since(Clock::time_point t0)
+{
+  return std::chrono::duration<double>(Clock::now() - t0).count();
+}
+
+void
+host_name(char* out, size_t len)
+{
+  if (gethostname(out, len) != 0)
+    std::snprintf(out, len, "?");
+  out[len - 1] = 0;
+}
+
+std::string
+ip_str(uint32_t addr_be)
+{
+  char b[INET_ADDRSTRLEN] = "?";
+  in_addr a;
+  a.s_addr = addr_be;
+  inet_ntop(AF_INET, &a, b, sizeof b);
+  return b;
+}
+
+// The address peers connect to: ST_COMM_ADDR, else the first IPv4 address
+// of NCCL_SOCKET_IFNAME's interface (a plain prefix), else of the first up
+// non-loopback interface (RCCL's own bootstrap choice), else 127.0.0.1.
+uint32_t
+advertised_addr()
+{
+  if (const char* e = std::getenv("ST_COMM_ADDR")) {
+    in_addr a;
+    if (inet_pton(AF_INET, e, &a) == 1)
+      return a.s_addr;
+  }
+  std::string want;
+  if (const char* e = std::getenv("NCCL_SOCKET_IFNAME"))
+    if (e[0] && e[0] != '^' && e[0] != '=')
+      want = std::string(e).substr(0, std::string(e).find(','));
+  uint32_t pick = htonl(INADDR_LOOPBACK);
+  ifaddrs* ifs = nullptr;
+  if (getifaddrs(&ifs) != 0)
+    return pick;
+  bool found = false;
+  for (int pass = want.empty() ? 1 : 0; pass < 2 && !found; pass++)
+    for (ifaddrs* i = ifs; i && !found; i = i->ifa_next) {
+      if (!i->ifa_addr || i->ifa_addr->sa_family != AF_INET)
+        continue;
+      if (!(i->ifa_flags & IFF_UP) || (i->ifa_flags & IFF_LOOPBACK))
+        continue;
+      if (pass == 0 && std::strncmp(i->ifa_name, want.c_str(), want.size()) != 0)
+        continue;
+      if (pass == 1 && std::strncmp(i->ifa_name, "docker", 6) == 0)
+        continue;
+      pick = reinterpret_cast<sockaddr_in*>(i->ifa_addr)->sin_addr.s_addr;
+      found = true;
+    }
+  freeifaddrs(ifs);
+  return pick;
+}
+
+// wait until fd is readable (POLLIN) or writable (POLLOUT), at most ms
+bool
+wait_fd(int fd, short ev, int ms)
+{
+  pollfd p{ fd, ev, 0 };
+  for (;;) {
+    const int r = poll(&p, 1, ms < 0 ? 0 : ms);
+    if (r < 0 && errno == EINTR)
+      continue;
+    return r > 0;
+  }
+}
+
+// read exactly len bytes before `until`; false on EOF, error or time-out
+bool
+read_all(int fd, void* buf, size_t len, Clock::time_point until)
+{
+  char* p = static_cast<char*>(buf);
+  while (len) {
+    const auto left =
+      std::chrono::duration_cast<std::chrono::milliseconds>(until - Clock::now())
+        .count();
+    if (left <= 0 || !wait_fd(fd, POLLIN, (int)std::min<long long>(left, 200)))
+    {
+      if (left <= 0)
+        return false;
+      continue;
+    }
+    const ssize_t r = recv(fd, p, len, 0);
+    if (r == 0)
+      return false;
+    if (r < 0) {
+      if (errno == EINTR || errno == EAGAIN || errno == EWOULDBLOCK)
+        continue;
+      return false;
+    }
+    p += r;
+    len -= (size_t)r;
+  }
+  return true;
+}
+
+bool
+write_all(int fd, const void* buf, size_t len)
+{
+  const char* p = static_cast<const char*>(buf);
+  while (len) {
+    const ssize_t r = send(fd, p, len, MSG_NOSIGNAL);
+    if (r < 0) {
+      if (errno == EINTR)
+        continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) {
+        wait_fd(fd, POLLOUT, 200);
+        continue;
+      }
+      return false;
+    }
+    p += r;
+    len -= (size_t)r;
+  }
+  return true;
+}
+
+std::string
+rank_list(const std::vector<int>& r)
+{
+  std::string s;
+  for (size_t i = 0; i < r.size(); i++)
+    s += (i ? ", " : "") + std::to_string(r[i]);
+  return s;
+}
+
+int
+reply_all(const std::vector<int>& fds, uint64_t nonce, int status,
+          const char* payload, const std::string& msg)
+{
+  Reply rp;
+  std::memset(&rp, 0, sizeof rp);
+  rp.nonce = nonce;
+  rp.status = status;
+  if (payload)
+    std::memcpy(rp.payload, payload, kRdvPayloadBytes);
+  std::snprintf(rp.msg, sizeof rp.msg, "%s", msg.c_str());
+  int bad = 0;
+  for (int fd : fds)
+    if (fd >= 0 && !write_all(fd, &rp, sizeof rp))
+      bad++;
+  return bad;
+}
+
+void
+close_all(std::vector<int>& fds)
+{
+  for (int& fd : fds)
+    if (fd >= 0) {
+      close(fd);
+      fd = -1;
+    }
+}
+
+// the host side: collect a hello from every other rank, then reply
+int
+host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
+          const std::function<int(char*)>& make_payload, char* payload)
+{
+  const auto t0 = Clock::now();
+  const auto until = t0 + std::chrono::duration_cast<Clock::duration>(
+                            std::chrono::duration<double>(limit));
+  std::vector<int> fds(nranks, -1); // fds[r]: rank r's connection
+  std::vector<Hello> who(nranks);
+  int present = 1;
+  std::string fail;
+  while (present < nranks && fail.empty()) {
+    const auto left =
+      std::chrono::duration_cast<std::chrono::milliseconds>(until - Clock::now())
+        .count();
+    if (left <= 0)
+      break;
+    if (!wait_fd(lfd, POLLIN, (int)std::min<long long>(left, 200)))
+      continue;
+    const int c = accept(lfd, nullptr, nullptr);
+    if (c < 0)
+      continue;
+    int one = 1;
+    setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+    Hello h;
+    // a hello follows the connect at once; 5 s covers a loaded host
+    const auto h_until = std::min(until, Clock::now() + std::chrono::seconds(5));
+    if (!read_all(c, &h, sizeof h, h_until) || h.nonce != id.nonce) {
+      close(c); // not one of ours (or it gave up): ignore it
+      continue;
+    }
+    h.host[sizeof h.host - 1] = 0;
+    if (h.nranks != nranks || h.rank < 0 || h.rank >= nranks || h.rank == rank ||
+        fds[h.rank] >= 0) {
+      char b[400];
+      std::snprintf(b, sizeof b,
+                    "rank %d (pid %d on %s) joined with nranks %d; the id's "
+                    "host is rank %d of %d%s",
+                    h.rank, h.pid, h.host, h.nranks, rank, nranks,
+                    (h.rank >= 0 && h.rank < nranks && fds[h.rank] >= 0) ||
+                        h.rank == rank
+                      ? " and that rank is already present"
+                      : "");
+      fail = b;
+      std::vector<int> one_fd{ c };
+      reply_all(one_fd, id.nonce, 2, nullptr, fail);
+      close(c);
+      break;
+    }
+    fds[h.rank] = c;
+    who[h.rank] = h;
+    present++;
+  }
+  if (fail.empty() && present < nranks) {
+    std::vector<int> missing, here{ rank };
+    for (int r = 0; r < nranks; r++)
+      if (r != rank) {
+        if (fds[r] < 0)
+          missing.push_back(r);
+        else
+          here.push_back(r);
+      }
+    std::sort(here.begin(), here.end());
+    char b[480];
+    std::snprintf(b, sizeof b,
+                  "RCCL rank%s %s of %d did not reach st_comm_init within %.1f s "
+                  "(ST_COMM_TIMEOUT_S / st_set_comm_timeout; present: %s; the "
+                  "id's host is rank %d on %s): no rank entered RCCL",
+                  missing.size() > 1 ? "s" : "", rank_list(missing).c_str(), nranks,
+                  seconds_since(t0), rank_list(here).c_str(), rank, id.host);
+    fail = b;
+  }
+  if (fail.empty() && make_payload(payload) != 0)
+    fail = std::string("the id's host (rank ") + std::to_string(rank) +
+           ") could not make the RCCL id";
+  if (fail.empty()) {
+    const int bad = reply_all(fds, id.nonce, 0, payload, "");
+    close_all(fds);
+    if (bad) {
+      ::st::set_error("st_comm_init: %d rank(s) closed the rendezvous before "
+                      "receiving the RCCL id",
+                      bad);
+      return -1;
+    }
+    return 0;
+  }
+  reply_all(fds, id.nonce, 1, nullptr, fail);
+  close_all(fds);
+  ::st::set_error("st_comm_init: %s", fail.c_str());
+  return -1;
+}
+
+// any other rank: connect, hello, wait for the host's reply
+int
+peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
+          char* payload)
+{
+  const auto t0 = Clock::now();
+  const auto until = t0 + std::chrono::duration_cast<Clock::duration>(
+                            std::chrono::duration<double>(limit));
+  const std::string where = ip_str(id.addr) + ":" + std::to_string(ntohs(id.port)) +
+                            " (" + id.host + ")";
+  int fd = -1;
+  while (fd < 0) {
+    if (Clock::now() >= until) {
+      ::st::set_error("st_comm_init: RCCL rank %d of %d could not reach the id's "
+                      "host at %s within %.1f s (ST_COMM_TIMEOUT_S / "
+                      "st_set_comm_timeout): the rank that made the id did not "
+                      "reach st_comm_init; no rank entered RCCL",
+                      rank, nranks, where.c_str(), seconds_since(t0));
+      return -1;
+    }
+    const int s = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
+    if (s < 0) {
+      ::st::set_error("st_comm_init: socket: %s", std::strerror(errno));
+      return -1;
+    }
+    sockaddr_in sa{};
+    sa.sin_family = AF_INET;
+    sa.sin_addr.s_addr = id.addr;
+    sa.sin_port = id.port;
+    int rc = connect(s, reinterpret_cast<sockaddr*>(&sa), sizeof sa);
+    if (rc < 0 && errno == EINPROGRESS && wait_fd(s, POLLOUT, 1000)) {
+      int err = 0;
+      socklen_t el = sizeof err;
+      getsockopt(s, SOL_SOCKET, SO_ERROR, &err, &el);
+      rc = err ? -1 : 0;
+    }
+    if (rc == 0) {
+      fd = s;
+    } else {
+      close(s);
+      std::this_thread::sleep_for(std::chrono::milliseconds(50));
+    }
+  }
+  int one = 1;
+  setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+  Hello h;
+  std::memset(&h, 0, sizeof h);
+  h.nonce = id.nonce;
+  h.nranks = nranks;
+  h.rank = rank;
+  h.device = device;
+  h.pid = (int32_t)getpid();
+  host_name(h.host, sizeof h.host);
+  if (!write_all(fd, &h, sizeof h)) {
+    close(fd);
+    ::st::set_error("st_comm_init: RCCL rank %d: the id's host at %s closed the "
+                    "rendezvous",
+                    rank, where.c_str());
+    return -1;
+  }
+  // the host answers when every rank is present or at ITS deadline, which
+  // may lie up to one deadline after this rank's: wait for the reply (and
+  // the names it carries) that much longer
+  const auto r_until = until + std::chrono::duration_cast<Clock::duration>(
+                                 std::chrono::duration<double>(limit));
+  Reply rp;
+  const bool got = read_all(fd, &rp, sizeof rp, r_until);
+  close(fd);
+  if (!got || rp.nonce != id.nonce) {
+    ::st::set_error("st_comm_init: RCCL rank %d of %d: no word from the id's host "
+                    "at %s after %.1f s (it failed, exited or never joined); no "
+                    "rank entered RCCL",
+                    rank, nranks, where.c_str(), seconds_since(t0));
+    return -1;
+  }
+  rp.msg[sizeof rp.msg - 1] = 0;
+  if (rp.status != 0) {
+    ::st::set_error("st_comm_init: %s", rp.msg);
+    return -1;
+  }
+  std::memcpy(payload, rp.payload, kRdvPayloadBytes);
+  return 0;
+}
+
+} // namespace
+
+int
+rdv_make_id(char* out)
+{
+  const int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  ST_REQUIRE(fd >= 0, "st_comm_unique_id: socket: %s", std::strerror(errno));
+  sockaddr_in sa{};
+  sa.sin_family = AF_INET;
+  sa.sin_addr.s_addr = htonl(INADDR_ANY);
+  sa.sin_port = 0;
+  socklen_t sl = sizeof sa;
+  if (bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0 ||
+      listen(fd, 1024) != 0 ||
+      getsockname(fd, reinterpret_cast<sockaddr*>(&sa), &sl) != 0) {
+    const int e = errno;
+    close(fd);
+    ::st::set_error("st_comm_unique_id: listener: %s", std::strerror(e));
+    return -1;
+  }
+  RdvId id;
+  std::memset(&id, 0, sizeof id);
+  std::memcpy(id.magic, kMagic, sizeof kMagic);
+  std::random_device rd;
+  id.nonce = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 16) ^
+             (uint64_t)Clock::now().time_since_epoch().count();
+  id.addr = advertised_addr();
+  id.port = sa.sin_port;
+  host_name(id.host, sizeof id.host);
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_listeners[id.nonce] = fd;
+  }
+  std::memset(out, 0, kRdvIdBytes);
+  std::memcpy(out, &id, sizeof id);
+  return 0;
+}
+
+int
+rdv_join(const char* id_in, int nranks, int rank, int device, double limit,
+         const std::function<int(char*)>& make_payload, char* payload)
+{
+  RdvId id;
+  std::memcpy(&id, id_in, sizeof id);
+  ST_REQUIRE(std::memcmp(id.magic, kMagic, sizeof kMagic) == 0,
+             "st_comm_init: the id was not made by st_comm_unique_id");
+  id.host[sizeof id.host - 1] = 0;
+  int lfd = -1;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_listeners.find(id.nonce);
+    if (it != g_listeners.end()) {
+      lfd = it->second;
+      g_listeners.erase(it);
+    }
+  }
+  if (lfd < 0)
+    return peer_join(id, nranks, rank, device, limit, payload);
+  // this process made the id: host the rendezvous, then close the listener
+  // (a rank arriving later is refused at connect and fails at its deadline)
+  const int rc = host_join(lfd, id, nranks, rank, limit, make_payload, payload);
+  close(lfd);
+  return rc;
+}
+
+} // namespace st

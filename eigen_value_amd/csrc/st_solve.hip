@@ -454,8 +454,8 @@ st_version(void)
   // the A/B probe switches the kernels were built with (st_kernels.hip):
   // "defaults" in every library build, the values in a probe build
   static const std::string v =
-    std::string("eigen_value_amd 0.4.0 (gfx950; probe switches: ") +
-    st_probe_switches() + ")";
+    std::string("eigen_value_amd 0.5.0 (gfx950; probe switches: ") +
+    st_probe_switches() + "; " + st::rccl_desc() + ")";
   return v.c_str();
 }
 

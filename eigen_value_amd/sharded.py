@@ -166,46 +166,129 @@ class HipShardOps:
         return self.dev.read_state(state)
 
 
+class PeerMissingError(_lib.EigenValueError):
+    """A rank did not reach the communicator rendezvous within the deadline.
+    Raised on every rank that did; ``missing`` lists the absent group ranks.
+    No RCCL state exists at that point, and no collective may be issued on
+    the group (it would wait for the absent rank)."""
+
+    def __init__(self, msg: str, missing):
+        super().__init__(msg)
+        self.missing = list(missing)
+
+
+_RDV_SEQ = [0]
+
+
+def _group_store(group):
+    """The process group's c10d store (keys of a sub-group are prefixed
+    with its global ranks, so groups do not collide)."""
+    import torch.distributed as dist
+    from torch.distributed import distributed_c10d as c10d
+    store = c10d._get_default_store()
+    if group is not None:
+        ranks = ",".join(str(dist.get_global_rank(group, r))
+                         for r in range(dist.get_world_size(group)))
+        store = dist.PrefixStore(f"g[{ranks}]/", store)
+    return store
+
+
+def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=None,
+               tag: str = "comm") -> Optional[bytes]:
+    """Every rank of `group` proves presence over the group's c10d store
+    (TCP, no collective) before any rank enters RCCL: each sets its key,
+    then waits at most `timeout` seconds (default: the library's RCCL
+    deadline, st_get_comm_timeout) for every other rank's.  A rank that
+    does not arrive makes every present rank raise PeerMissingError naming
+    it - instead of the first RCCL call (init, or torch's broadcast of the
+    id) waiting for it indefinitely.
+
+    payload_from_first: called on group rank 0 once everyone is present; its
+    bytes (or an exception's text) reach every rank, which returns them.
+    Calls are matched across ranks by order: every rank must make the same
+    sequence of rendezvous calls on a group."""
+    import datetime
+
+    import torch.distributed as dist
+    if timeout is None:
+        timeout = _lib.load().st_get_comm_timeout()
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    _RDV_SEQ[0] += 1
+    base = f"eigen_value_amd/rdv/{tag}/{_RDV_SEQ[0]}"
+    store = _group_store(group)
+    store.set(f"{base}/here/{rank}", b"1")
+    keys = [f"{base}/here/{r}" for r in range(world)]
+    try:
+        store.wait(keys, datetime.timedelta(seconds=timeout))
+    except Exception as e:  # noqa: BLE001 - c10d raises DistStoreError/RuntimeError
+        missing = [r for r in range(world) if not store.check([keys[r]])]
+        if not missing:       # everyone arrived as the wait gave up
+            missing = None
+        if missing is not None:
+            raise PeerMissingError(
+                f"group rank{'s' if len(missing) > 1 else ''} "
+                f"{', '.join(map(str, missing))} of {world} did not reach the communicator "
+                f"rendezvous within {timeout:.1f} s (st_set_comm_timeout / "
+                f"ST_COMM_TIMEOUT_S); this is rank {rank}; no rank entered RCCL",
+                missing) from e
+    if payload_from_first is None:
+        return None
+    key = f"{base}/payload"
+    if rank == 0:
+        try:
+            data = b"ok:" + bytes(payload_from_first())
+        except Exception as e:  # noqa: BLE001 - reaches every rank below
+            data = b"error:" + f"{type(e).__name__}: {e}".encode()
+        store.set(key, data)
+    else:
+        store.wait([key], datetime.timedelta(seconds=timeout))
+        data = store.get(key)
+    if data.startswith(b"error:"):
+        raise _lib.EigenValueError(f"group rank 0 failed: {data[6:].decode(errors='replace')}")
+    return data[3:]
+
+
 class RcclComm:
     """An RCCL communicator owned by libsimilarity_transform.so for the
-    per-round all-gather: the unique id is made by rank 0 and broadcast over
-    the existing torch.distributed group; the collective is then issued
-    straight on the launch stream (no per-round hand-off between torch's
-    compute and communication streams)."""
+    per-round all-gather: every rank proves presence over the group's c10d
+    store (rendezvous), group rank 0 then makes the library's id and hands
+    it over the store, and every rank joins with st_comm_init (which checks
+    presence once more before RCCL is entered, st_rendezvous.hip); the
+    collective is then issued straight on the launch stream (no per-round
+    hand-off between torch's compute and communication streams)."""
 
-    def __init__(self, group=None, device_index: Optional[int] = None):
+    def __init__(self, group=None, device_index: Optional[int] = None,
+                 timeout: Optional[float] = None):
         import ctypes
 
         import torch
         import torch.distributed as dist
         self.ctypes, self.torch = ctypes, torch
         self.L = _lib.load()
+        self.comm = ctypes.c_void_p()
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         dev = torch.cuda.current_device() if device_index is None else device_index
-        uid = ctypes.create_string_buffer(128)
-        # rank 0's failure to make an id reaches every rank (its error text
-        # is broadcast instead of the id), so no rank enters st_comm_init
-        obj = [None]
-        if rank == 0:
-            obj = ([uid.raw] if self.L.st_comm_unique_id(uid) == 0
-                   else [("error", _lib.last_error())])
-        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group else 0,
-                                   group=group)
-        self.comm = ctypes.c_void_p()
-        if isinstance(obj[0], tuple):
-            raise _lib.EigenValueError(f"st_comm_unique_id failed on rank 0: {obj[0][1]}")
-        _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, obj[0], dev),
+
+        def make_id():
+            uid = ctypes.create_string_buffer(128)
+            _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
+            return uid.raw
+
+        uid = rendezvous(group, timeout, payload_from_first=make_id)
+        _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, uid, dev),
                    "st_comm_init")
         self.rank, self.world = rank, world
 
     def info(self) -> dict:
-        """What RCCL itself reports for this communicator (st_comm_info)."""
+        """What RCCL itself reports for this communicator (st_comm_info),
+        and which RCCL this process's library calls are bound to."""
         ctypes = self.ctypes
         n, r, d = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
         _lib.check(self.L.st_comm_info(self.comm, ctypes.byref(n), ctypes.byref(r),
                                        ctypes.byref(d)), "st_comm_info")
-        return {"nranks": n.value, "rank": r.value, "device": d.value}
+        return {"nranks": n.value, "rank": r.value, "device": d.value,
+                **_lib.rccl_info(self.L)}
 
     def allgather(self, out, inp) -> None:
         sfx = "f64" if out.dtype == self.torch.float64 else "f32"
@@ -219,9 +302,10 @@ class RcclComm:
             self.comm = self.ctypes.c_void_p()
 
 
-# set when st_comm_init reported that RCCL's abort left its init thread
-# blocked (st_multi.hip init_with_deadline): the process should end with
-# os._exit, since a normal exit can crash in the runtimes' teardown behind it
+# set when st_comm_init reported that its RCCL init thread is left behind (a
+# peer died between the rendezvous and the init, st_multi.hip
+# init_with_deadline): the process should end with os._exit, since a normal
+# exit can crash in the runtimes' teardown behind it
 INIT_THREAD_LEFT_BEHIND = False
 
 
@@ -230,20 +314,24 @@ def make_comm_agreed(group, factory, device=None):
     whether it succeeded: a communicator is used only if EVERY rank has one
     - otherwise all ranks close theirs and return (None, reason), so no rank
     issues the library all-gather while another waits in torch's (a mixed
-    exchange would hang the first round).  Every rank reaches the
-    all-reduce: rank 0's id failure is broadcast before anyone joins, and a
-    rank whose st_comm_init fails leaves its peers waiting only until the
-    library's RCCL deadline (st_set_comm_timeout, ST_COMM_TIMEOUT_S), after
-    which their st_comm_init aborts and returns an error too."""
+    exchange would hang the first round).  A rank missing from the
+    rendezvous (PeerMissingError) is re-raised instead: no collective on the
+    group can complete without it, the all-reduce included.  Every present
+    rank reaches the all-reduce otherwise: rank 0's id failure reaches all
+    ranks through the store, and st_comm_init fails on all ranks alike."""
     import torch
     import torch.distributed as dist
     global INIT_THREAD_LEFT_BEHIND
     comm, err = None, None
     try:
         comm = factory()
+    except PeerMissingError:
+        raise
     except Exception as e:  # noqa: BLE001 - agreed on below
         err = f"{type(e).__name__}: {e}"
-        if "left behind" in err:
+        if "no rank entered RCCL" in err:   # st_comm_init's rendezvous: a rank is absent
+            raise PeerMissingError(err, []) from e
+        if "_exit" in err:
             INIT_THREAD_LEFT_BEHIND = True
     flag = torch.tensor([0 if comm is None else 1], dtype=torch.int32,
                         device=device if device is not None else "cpu")

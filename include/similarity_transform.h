@@ -181,19 +181,33 @@ int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
                            unsigned int* iter_cnt, const st_options* opt,
                            st_stats* stats);
 
-/* One-process-per-GPU RCCL communicator for the sharded step API: rank 0
- * calls st_comm_unique_id (128 bytes), the caller distributes the id, every
- * rank calls st_comm_init (nranks, its rank, its HIP device).  st_allgather
- * is ncclAllGather on `stream` (in place when send = recv + rank*count).
+/* One-process-per-GPU RCCL communicator for the sharded step API: one
+ * process calls st_comm_unique_id (ST_COMM_ID_BYTES), the caller
+ * distributes the id, every rank calls st_comm_init (nranks, its rank, its
+ * HIP device); the process that made the id must join too.  st_allgather is
+ * ncclAllGather on `stream` (in place when send = recv + rank*count).
+ *
+ * Presence before RCCL: the id is a rendezvous id, not an RCCL one - the
+ * maker listens on a TCP port (address: ST_COMM_ADDR, else the first IPv4
+ * address of NCCL_SOCKET_IFNAME's or of the first up non-loopback
+ * interface, else 127.0.0.1).  st_comm_init on every rank first joins it;
+ * only when all nranks are present does the maker create the RCCL id and
+ * hand it to all, and only then does any rank enter ncclCommInitRankConfig.
+ * A rank that does not arrive within the deadline makes st_comm_init return
+ * -1 on every present rank, eigen_last_error() naming the missing ranks,
+ * with no RCCL state created (the process exits normally).
  *
  * Deadline: every communicator is non-blocking (ncclConfig_t.blocking = 0)
- * and each step that waits for peers - st_comm_init, a collective's
- * connection setup, st_comm_destroy, and the communicator setup and
- * all-gathers of st_solve_multi_* - is polled (ncclCommGetAsyncError) for at
- * most st_set_comm_timeout() seconds (default: the environment variable
- * ST_COMM_TIMEOUT_S, else 120).  Past it the communicator is aborted
- * (ncclCommAbort) and the call returns -1; eigen_last_error() names the
- * RCCL rank and HIP device still in progress. */
+ * and each step that waits for peers - the rendezvous, st_comm_init's RCCL
+ * init, a collective's connection setup, st_comm_destroy, and the
+ * communicator setup and all-gathers of st_solve_multi_* - waits at most
+ * st_set_comm_timeout() seconds (default: the environment variable
+ * ST_COMM_TIMEOUT_S, else 120).  Past it the call returns -1 naming the RCCL
+ * rank and HIP device still in progress; a communicator whose init has
+ * returned is aborted (ncclCommAbort), one whose init has not is left to
+ * the init thread, which aborts it if the init ever returns (the error then
+ * says to end the process with _exit: a peer died after the rendezvous). */
+#define ST_COMM_ID_BYTES 128
 int st_comm_unique_id(char* id_out);
 int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
                  int device);
@@ -201,6 +215,15 @@ int st_comm_destroy(void* comm);
 /* Set the RCCL deadline in seconds (<= 0: back to ST_COMM_TIMEOUT_S / 120);
  * returns the previous effective value.  Process-wide. */
 double st_set_comm_timeout(double seconds);
+/* The effective RCCL deadline in seconds (the setter's, ST_COMM_TIMEOUT_S or
+ * 120). */
+double st_get_comm_timeout(void);
+/* The RCCL the library's calls are bound to: *version_code = ncclGetVersion
+ * (X*10000 + Y*100 + Z) and `path` = the file holding the bound
+ * ncclAllGather (dladdr); inside a torch process that is torch's bundled
+ * librccl, for a C caller the /opt/rocm one the library links.  Either
+ * output may be NULL.  Returns 0 or -1.  No GPU needed. */
+int st_rccl_version(int* version_code, char* path, int path_len);
 /* What the communicator itself reports (ncclCommCount / ncclCommUserRank /
  * ncclCommCuDevice): the ranks RCCL joined, this rank, its HIP device.
  * Any output pointer may be NULL.  Returns 0 or negative. */
@@ -597,9 +620,10 @@ int st_epilogue_f64(const double* d_s, double* d_v, unsigned int n,
                     double eps, unsigned int max_itr, unsigned int semantics,
                     st_state* d_state, void* stream);
 
-/* Library / device facts.  st_version names the library, the target and
- * the A/B probe switches its kernels were built with ("defaults" in every
- * library build; st_probe_switches returns that part alone). */
+/* Library / device facts.  st_version names the library, the target, the
+ * A/B probe switches its kernels were built with ("defaults" in every
+ * library build; st_probe_switches returns that part alone) and the RCCL
+ * its calls are bound to (st_rccl_version). */
 const char* st_version(void);
 const char* st_probe_switches(void);
 int st_device_count(void);

@@ -124,6 +124,26 @@ def test_stalled_ranks_are_ended_by_the_parent_deadline():
     assert el < 200
 
 
+def test_stalled_rank_is_named_by_the_communicator_rendezvous():
+    """--stall-rank 1 --stall-in rendezvous: ranks 0 and 2 of a gloo world 3
+    make the library communicator's presence check (sharded.rendezvous, the
+    step before any rank enters RCCL) and name rank 1 within --comm-timeout
+    (3 s), then the run ends non-zero without a JSON line."""
+    import time
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.time()
+    out = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "3",
+                          "--backend", "gloo", "--stall-rank", "1", "--stall-in", "rendezvous",
+                          "--comm-timeout", "3", "--stall-timeout", "120"],
+                         capture_output=True, text=True, timeout=240, cwd=REPO, env=env)
+    el = time.time() - t0
+    assert out.returncode != 0, out.stderr[-3000:]
+    assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert "group rank 1 of 3 did not reach the communicator rendezvous within 3.0 s" \
+        in out.stderr, out.stderr[-3000:]
+    assert el < 100
+
+
 @pytest.mark.gpu
 def test_bench_self_spawned_two_ranks_on_one_gpu():
     """The N > 1 line without torch.distributed.run: two self-spawned ranks

@@ -120,32 +120,53 @@ def test_config3_sharded_p1_vs_oracle():
 
 
 # ---------------------------------------------------------------------------
-# every device the box has (8 on the driver's node, 1 here)
+# P = 2, 4 and every device the box has (8 on the driver's node); on a box
+# with fewer devices those counts stay collected, skipped, with P in the id
 # ---------------------------------------------------------------------------
+def _multi_counts():
+    """P in {2, 4, NDEV} (and 8, the driver's node) ∩ [2, NDEV]; counts the
+    box lacks are skipped params whose id names the count."""
+    out = []
+    for p in sorted({2, 4, 8} | ({NDEV} if NDEV > 1 else set())):
+        if p <= NDEV and (p in (2, 4) or p == NDEV):
+            out.append(pytest.param(p, id=f"P{p}"))
+        elif p > NDEV:
+            out.append(pytest.param(p, id=f"P{p}-skipped-needs-{p}-devices",
+                                    marks=pytest.mark.skip(reason=f"needs >= {p} HIP devices, "
+                                                                  f"this box has {NDEV}")))
+    return out
+
+
 def _device_counts():
-    if NDEV > 1:
-        return [1, NDEV]
-    return [1, pytest.param(2, id="ngpus2-skipped-needs-2-devices",
-                            marks=pytest.mark.skip(reason=f"needs >= 2 HIP devices, "
-                                                          f"this box has {NDEV}"))]
+    return [pytest.param(1, id="P1")] + _multi_counts()
 
 
 @pytest.mark.parametrize("ngpus", _device_counts())
 def test_native_multi_gpu_all_devices(orc, ngpus):
-    """st_solve_multi_* over `ngpus` devices (ncclCommInitAll, one all-gather
-    per round) vs the oracle: a k_round block size and a flat-round
-    (deferred-write) block size."""
+    """st_solve_multi_* over `ngpus` devices (ncclCommInitAll, one grouped
+    all-gather per round) vs the oracle: a k_round block size (3001, the
+    oracle run here) and a flat-round (deferred-write) block size (32768²
+    random fp64 seed 0, 32768/P rows per device, vs the committed oracle pin
+    tests/golden/large_oracle.json: no host oracle at full size)."""
     from eigen_value_amd.multi import solve_multi
-    for n in (3001, 9216 * max(1, ngpus // 2)):
-        mat = orc.random_matrix(n, 3) if n <= 12000 else orc.generate_c("random", n, 3)
-        ref = orc.similarity_transform(mat, orc.SEM_SYCL, nthreads=HOST_THREADS)
-        del mat
-        lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=3)
-        assert it == ref.iter_count and st["rounds"] == ref.rounds_evaluated, n
-        assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
-        assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
-        r2 = solve_multi(n, "random", ngpus=ngpus, seed=3, write_every_round=True)
-        assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
+    n = 3001
+    ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL, nthreads=HOST_THREADS)
+    lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=3)
+    assert it == ref.iter_count and st["rounds"] == ref.rounds_evaluated, n
+    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
+    assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
+    r2 = solve_multi(n, "random", ngpus=ngpus, seed=3, write_every_round=True)
+    assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
+    pin, v_pin = large_oracle("random32768_f64")
+    n = 32768
+    lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=0)
+    assert it == pin["iter_count"] == 3 and st["rounds"] == pin["rounds_evaluated"]
+    assert abs(lam - pin["eigen_val"]) <= 1e-10 * pin["eigen_val"]
+    assert np.max(np.abs(v - v_pin)) <= 1e-10
+    r2 = solve_multi(n, "random", ngpus=ngpus, seed=0, write_every_round=True)
+    assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
+    del v, r2
+    _free()
 
 
 def _comm_worker(rank, world, port, outdir):
@@ -181,10 +202,7 @@ def _comm_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [NDEV] if NDEV > 1 else [
-    pytest.param(2, id="world2-skipped-needs-2-devices",
-                 marks=pytest.mark.skip(reason=f"RCCL needs one device per rank; "
-                                               f"this box has {NDEV}"))])
+@pytest.mark.parametrize("world", _multi_counts())
 def test_library_comm_all_devices(tmp_path, orc, world):
     """The library-owned RCCL communicator (st_comm_*) with nranks = every
     device: RCCL reports that many ranks, the in-slot all-gather is right,
@@ -252,15 +270,12 @@ def _config3_worker(rank, world, port, outdir):
             np.save(os.path.join(outdir, "v.npy"), v.cpu().numpy())
         np.save(os.path.join(outdir, f"r{rank}.npy"),
                 np.array([info["nranks"], info["rank"], info["device"], lam, it, rounds,
-                          sh.part.nrows]))
+                          sh.part.nrows, info["rccl_version_code"]]))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [NDEV] if NDEV > 1 else [
-    pytest.param(2, id="world2-skipped-needs-2-devices",
-                 marks=pytest.mark.skip(reason=f"RCCL needs one device per rank; "
-                                               f"this box has {NDEV}"))])
+@pytest.mark.parametrize("world", _multi_counts())
 def test_config3_one_process_per_gpu_vs_pin(tmp_path, world):
     """BASELINE configs[3] as the driver's scaling run shards it: one process
     per GPU (mp.spawn), ShardedSimilarityTransform(comm="native") - the
@@ -273,8 +288,9 @@ def test_config3_one_process_per_gpu_vs_pin(tmp_path, world):
     mp.spawn(_config3_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
     devices = set()
     for r in range(world):
-        nranks, rk, device, lam, it, rounds, nrows = np.load(tmp_path / f"r{r}.npy")
+        nranks, rk, device, lam, it, rounds, nrows, rccl = np.load(tmp_path / f"r{r}.npy")
         assert (int(nranks), int(rk)) == (world, r) and int(nrows) == 65536 // world
+        assert int(rccl) >= 22000         # the RCCL the ranks' library calls bound to
         devices.add(int(device))
         _check_config3(float(lam), np.load(tmp_path / "v.npy"), int(it), int(rounds))
     assert len(devices) == world
@@ -287,6 +303,7 @@ def test_config3_one_process_per_gpu_vs_pin(tmp_path, world):
 _DEADLINE_PROBE = r"""
 import ctypes, sys, time
 sys.path.insert(0, sys.argv[1])
+import torch                      # as in a torch process: torch's RCCL is the one bound
 from eigen_value_amd import _lib
 L = _lib.load()
 L.st_set_comm_timeout(3.0)
@@ -296,32 +313,87 @@ comm = ctypes.c_void_p()
 t0 = time.time()
 rc = L.st_comm_init(ctypes.byref(comm), 2, 0, uid.raw, 0)   # rank 1 never joins
 print("RC", rc, "EL", round(time.time() - t0, 2), "NULL", comm.value is None)
-print("ERR", _lib.last_error(), flush=True)
-# a job that lost a peer ends; with _exit, as bench.py's watchdog does: a
-# normal exit can crash in the runtimes' teardown behind an init thread
-# RCCL's abort did not unblock (the error message says whether it did)
-import os
-os._exit(0)
+print("ERR", _lib.last_error())
+print("RCCL", _lib.rccl_info()["rccl_version"], flush=True)
 """
 
 
 def test_comm_init_deadline_names_the_stalled_rank(tmp_path):
-    """st_comm_init as rank 0 of 2 with no rank 1: the non-blocking init is
-    polled for the 3 s deadline, then aborted; the call returns -1, leaves
-    the handle NULL and eigen_last_error names rank 0 / device 0 (VERDICT r03
-    'next' #1).  In a child process, bounded, so a hang cannot take the
-    test runner with it."""
+    """st_comm_init as rank 0 of 2 with no rank 1: the presence check before
+    RCCL (st_rendezvous.hip) waits the 3 s deadline, returns -1, leaves the
+    handle NULL and names rank 1; no rank entered RCCL, so the process ends
+    with a NORMAL interpreter exit and returncode 0 (round 4
+    entered RCCL's init, whose abort left a thread that crashed the exit).
+    In a child process, bounded, so a hang cannot take the test runner."""
     import subprocess
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     out = subprocess.run([sys.executable, "-c", _DEADLINE_PROBE, repo], capture_output=True,
                          text=True, timeout=150)
-    assert out.returncode == 0, out.stderr[-3000:]
-    lines = dict(ln.split(" ", 1) for ln in out.stdout.splitlines() if ln[:3] in ("RC ", "ERR"))
+    assert out.returncode == 0, (out.returncode, out.stdout[-2000:], out.stderr[-3000:])
+    lines = dict(ln.split(" ", 1) for ln in out.stdout.splitlines()
+                 if ln[:3] in ("RC ", "ERR") or ln.startswith("RCCL "))
     rc, _, el, _, null = lines["RC"].split()
     assert int(rc) < 0 and null == "True"
-    assert 3.0 <= float(el) < 30.0        # the deadline + at most 10 s for the helper
-    assert "still in progress" in lines["ERR"] and "rank 0 (device 0)" in lines["ERR"]
+    assert 3.0 <= float(el) < 10.0
+    assert "RCCL rank 1 of 2 did not reach st_comm_init" in lines["ERR"], lines["ERR"]
+    assert "no rank entered RCCL" in lines["ERR"]
+    print("probe:", lines)
+
+
+_SAME_DEVICE_PROBE = r"""
+import ctypes, os, sys, time
+sys.path.insert(0, sys.argv[1])
+import torch
+from eigen_value_amd import _lib
+mode, idfile = sys.argv[2], sys.argv[3]
+L = _lib.load()
+L.st_set_comm_timeout(30.0)
+if mode == "host":
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id(uid) == 0
+    open(idfile + ".tmp", "w").write(uid.raw.hex())
+    os.replace(idfile + ".tmp", idfile)
+    raw, rank = uid.raw, 0
+else:
+    while not os.path.exists(idfile):
+        time.sleep(0.05)
+    raw, rank = bytes.fromhex(open(idfile).read()), 1
+comm = ctypes.c_void_p()
+t0 = time.time()
+rc = L.st_comm_init(ctypes.byref(comm), 2, rank, raw, 0)
+print("RC", rc, "EL", round(time.time() - t0, 2), flush=True)
+print("ERR", _lib.last_error(), flush=True)
+if rc == 0:
+    print("DESTROY", L.st_comm_destroy(comm), flush=True)
+"""
+
+
+def test_comm_init_two_ranks_one_device_exit_normally(tmp_path):
+    """Two processes join one rendezvous as ranks 0 and 1, both on device 0:
+    the presence check passes and both enter ncclCommInitRankConfig, which
+    RCCL refuses for a device used twice (profiles/r04_rccl_same_gpu_probe.log)
+    - or accepts; either way the init thread reports, owns and aborts the
+    failed communicator itself, the call returns promptly, and BOTH
+    processes end with a normal exit, returncode 0 (the single-owner init,
+    ADVICE r04 st_multi.hip:194)."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    idfile = str(tmp_path / "id")
+    procs = [subprocess.Popen([sys.executable, "-c", _SAME_DEVICE_PROBE, repo, m, idfile],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for m in ("host", "peer")]
+    outs = [p.communicate(timeout=150) for p in procs]
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, (p.returncode, so[-2000:], se[-3000:])
+        lines = dict(ln.split(" ", 1) for ln in so.splitlines() if ln[:3] in ("RC ", "ERR"))
+        rc, _, el = lines["RC"].split()
+        assert float(el) < 60.0
+        assert "did not reach" not in lines["ERR"] and "no word" not in lines["ERR"]
+        if int(rc) < 0:
+            assert "ncclCommInitRankConfig" in lines["ERR"], lines["ERR"]
+        print("probe:", lines)
 
 
 _DUPLICATE_PROBE = r"""

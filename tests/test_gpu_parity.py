@@ -864,10 +864,15 @@ def _rccl_worker(rank, port, outdir):
         out = torch.arange(12, dtype=torch.float64, device="cuda")
         _allgather(out, out[0:12])
         assert torch.equal(out, torch.arange(12, dtype=torch.float64, device="cuda"))
-        # the library-owned communicator (id broadcast over the group)
+        # the library-owned communicator (presence and id over the group's
+        # store, then st_comm_init's own rendezvous)
         from eigen_value_amd.sharded import RcclComm
         rc = RcclComm()
-        assert rc.info() == {"nranks": 1, "rank": 0, "device": 0}
+        info = rc.info()
+        assert {k: info[k] for k in ("nranks", "rank", "device")} == \
+            {"nranks": 1, "rank": 0, "device": 0}
+        # in a torch process the library's RCCL calls bind torch's bundled RCCL
+        assert "torch" in info["rccl_path"] and info["rccl_version_code"] >= 22000, info
         for dt in (torch.float64, torch.float32):
             out = torch.arange(12, dtype=dt, device="cuda")
             rc.allgather(out, out[0:12])

@@ -592,3 +592,90 @@ def test_library_comm_is_used_only_if_every_rank_has_one(tmp_path, fail_rank):
             assert closed == (0 if r == fail_rank else 1)    # the others closed theirs
         # the failing rank knows to end with _exit (bench.py does)
         assert bool(left) == (r == fail_rank)
+
+
+# ---------------------------------------------------------------------------
+# the library communicator's presence check (sharded.rendezvous): over the
+# group's c10d store, before any rank enters RCCL
+# ---------------------------------------------------------------------------
+def _rdv_worker(rank, world, port, stall_rank, outdir):
+    import time
+
+    from eigen_value_amd import sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    res = {"rank": rank}
+    try:
+        if rank == stall_rank:
+            time.sleep(6.0)            # never calls: a rank stuck before the communicator
+        else:
+            t0 = time.time()
+            try:
+                res["payload"] = sharded.rendezvous(
+                    None, 2.0, payload_from_first=lambda: b"id-bytes").decode()
+            except sharded.PeerMissingError as e:
+                res.update(missing=e.missing, msg=str(e))
+            res["el"] = time.time() - t0
+            # a second rendezvous on the same group (the next communicator)
+            # is matched by order and does not see the first one's keys
+            if stall_rank < 0:
+                def boom():
+                    raise RuntimeError("no id today")
+                try:
+                    sharded.rendezvous(None, 5.0, payload_from_first=boom)
+                except _lib.EigenValueError as e:
+                    res["second"] = str(e)
+        import json
+        with open(os.path.join(outdir, f"rdv{rank}.json"), "w") as f:
+            json.dump(res, f)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("stall_rank", [-1, 1])
+def test_rendezvous_names_the_missing_rank(tmp_path, stall_rank):
+    """gloo world 3.  All present: every rank returns group rank 0's payload
+    (the library id), and a payload failure reaches every rank as an error.
+    Rank 1 absent: ranks 0 and 2 raise PeerMissingError naming rank 1 within
+    the 2 s deadline (not after a hang in RCCL init or torch's broadcast)."""
+    import json
+    mp.spawn(_rdv_worker, args=(3, _free_port(), stall_rank, str(tmp_path)), nprocs=3,
+             join=True)
+    for r in range(3):
+        res = json.load(open(tmp_path / f"rdv{r}.json"))
+        if r == stall_rank:
+            continue
+        if stall_rank < 0:
+            assert res["payload"] == "id-bytes" and res["el"] < 5.0
+            assert "group rank 0 failed: RuntimeError: no id today" in res["second"]
+        else:
+            assert res["missing"] == [1], res
+            assert "group rank 1 of 3 did not reach the communicator rendezvous" in res["msg"]
+            assert 2.0 <= res["el"] < 5.5, res
+
+
+def _agree_missing_worker(rank, world, port, outdir):
+    from eigen_value_amd import sharded
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        def factory():
+            # as RcclComm reports a rank absent from st_comm_init's rendezvous
+            raise _lib.EigenValueError("st_comm_init failed: st_comm_init: RCCL rank 1 of 2 "
+                                       "did not reach st_comm_init within 2.0 s (...): "
+                                       "no rank entered RCCL")
+        try:
+            sharded.make_comm_agreed(None, factory)
+            out = "returned"
+        except sharded.PeerMissingError:
+            out = "raised"
+        open(os.path.join(outdir, f"m{rank}"), "w").write(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_make_comm_agreed_does_not_all_reduce_past_a_missing_rank(tmp_path):
+    """A missing rank is re-raised by make_comm_agreed, not taken into its
+    all-reduce (which would wait for the absent rank forever)."""
+    mp.spawn(_agree_missing_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    assert [open(tmp_path / f"m{r}").read() for r in range(2)] == ["raised", "raised"]

@@ -1,0 +1,28 @@
+# round-5 GPU session steps (S=r05_sN STEPS="…" bash tools/session_r05.sh)
+set -u
+O=gpurun_out/${S:-r05_s1}; mkdir -p $O
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+fail() { echo "== stopping: $1 exited $2"; exit $2; }
+run() { # name secs cmd...  (rc 0/1 continue; anything else ends the session)
+  local n=$1 t=$2; shift 2
+  echo "== $n: $*"; local t0=$(date +%s)
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "== $n rc=$rc ($(( $(date +%s) - t0 ))s)"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then fail $n $rc; fi
+}
+for step in ${STEPS:-tests smoke bench}; do case $step in
+comm) run comm_tests 400 python3 -u -m pytest -x -v -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fullsize.py -k "comm_init or grouped_init or all_devices or config3"; tail -40 $O/comm_tests.log ;;
+tests) run pytest_gpu 900 python3 -u -m pytest -x -q -rs --timeout 300 --timeout-method thread -m gpu tests/; tail -15 $O/pytest_gpu.log ;;
+smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -3 $O/smoke.log ;;
+bench) run bench 900 python3 bench.py; tail -c 1500 $O/bench.log ;;
+benchquick) run benchquick 600 python3 bench.py --no-cpu --no-north-star --no-headline; tail -c 2500 $O/benchquick.log ;;
+prof)
+  D=$O/prof; mkdir -p $D
+  run prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --no-cpu --no-north-star --no-headline
+  head -12 $D/run_kernel_stats.csv ;;
+rcclchar)
+  # RCCL deadline behaviour on torch's bundled RCCL (a crash at exit is the finding)
+  timeout -k 5 40 python3 tools/rccl_deadline_torch.py --abort 0 > $O/rcclchar_noabort.log 2>&1; echo "rcclchar_noabort rc=$?"; grep "^\[" $O/rcclchar_noabort.log
+  timeout -k 5 40 python3 tools/rccl_deadline_torch.py --abort 1 > $O/rcclchar_abort.log 2>&1; echo "rcclchar_abort rc=$?"; grep "^\[" $O/rcclchar_abort.log ;;
+*) echo "unknown step $step"; exit 2 ;;
+esac; done
