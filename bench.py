@@ -469,19 +469,34 @@ def deferred_bitwise(sh, kind, seed, torch):
 
 
 def profile_cycle_ms(workload: str):
-    """Sum over one store cycle of the committed rocprof averages of the
-    deferred flat round (k_flat per pending count NP + k_parts per round),
-    from profiles/*_defer_cycle_*.json (tools/defer_profile.py --json)."""
+    """The committed rocprof kernel time per round of the deferred-write
+    loop for `workload`, from a kernel trace of this bench's own deferred
+    leg (profiles/*_defer_bench_*.json, tools/defer_profile.py --bench-leg:
+    k_flat + k_parts of the timed cycles, median pass of 3, each from a
+    fresh A_0 - the procedure the leg times with HIP events).  The latest
+    round's file wins; (ms per round, path) or None."""
     import glob
     best = None
-    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_defer_cycle_*.json"))):
+    for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_defer_bench_*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("workload") == workload:
-            best = (d["cycle_ms_per_round"], os.path.relpath(f, HERE))
+        for blk in d.get("blocks", []):
+            if blk.get("workload") == workload:
+                best = (blk["rocprof_ms_per_round"], os.path.relpath(f, HERE))
     return best
+
+
+def add_rocprof(out: dict, workload: str, ev_ms: float, by: float) -> None:
+    """The rocprof figure of the same procedure beside a deferred leg's
+    HIP-event one (profile_cycle_ms), and its roofline fraction."""
+    prof = profile_cycle_ms(workload)
+    if prof is not None:
+        out["rocprof_ms_per_round"] = prof[0]
+        out["rocprof_frac"] = round(rate(by, prof[0]) / HBM_PEAK_GBS, 4)
+        out["rocprof_source"] = prof[1]
+        out["events_vs_rocprof"] = round(ev_ms / prof[0], 4)
 
 
 # ---------------------------------------------------------------------------
@@ -600,6 +615,7 @@ def rank_block_legs(sharded, torch, cases, kind, steps, warmup, representative):
                                     "achieved": round(rate(by_d, ev_d), 1)}
             if representative:
                 r["deferred_writes"]["frac"] = round(rate(by_d, ev_d) / HBM_PEAK_GBS, 4)
+                add_rocprof(r["deferred_writes"], f"{kind}{n}_p{P}_f64", ev_d, by_d)
         out[f"P{P}"] = r
         sh.close()
         del sh
@@ -615,14 +631,22 @@ def deferred_leg(sharded, dev, torch, kind, n, dt, seed, every_ms):
     sh = sharded.ShardedSimilarityTransform(n, dt)
     if not sh.deferred_writes:
         return None
-    sh.load(kind, seed=seed)
     cycles = max(3, int(round(60.0 / max(every_ms, 1e-3) / 6)))  # ~40-60 ms of rounds
-    # three passes over the same number of whole cycles (the first after 2
-    # warm-up cycles), the median by HIP events: the rounds with pending
-    # scalings are issue-bound and follow the clock, which drifts by a few
-    # per cent over a bench run
-    runs = sorted((timed_deferred(sh, cycles, 2 if i == 0 else 0, torch, None, 1)
-                   for i in range(3)), key=lambda r: r[1])
+    # three passes over the same number of whole cycles, the median by HIP
+    # events (the rounds with pending scalings are issue-bound and follow the
+    # clock, which drifts by a few per cent over a bench run); every pass
+    # from a fresh A_0 with 2 warm-up cycles, so that each times the same
+    # data (on memory-side-cache-assisted blocks the streaming rate depends
+    # on the values, profiles/r03_data_dependence.log: round 4 ran passes 2
+    # and 3 on from pass 1's matrix, and its rocprof source - another
+    # process, other data - read 5 % slower).  The committed
+    # rocprof source is a kernel trace of THIS leg (tools/defer_profile.py
+    # --bench-leg), summarised the same way: median pass, timed cycles only
+
+    def one_pass():
+        sh.load(kind, seed=seed)
+        return timed_deferred(sh, cycles, 2, torch, None, 1)
+    runs = sorted((one_pass() for _ in range(3)), key=lambda r: r[1])
     el, ev_ms, m = runs[1]
     same = deferred_bitwise(sh, kind, seed, torch)
     bpe = 8 if dt == torch.float64 else 4
@@ -637,12 +661,9 @@ def deferred_leg(sharded, dev, torch, kind, n, dt, seed, every_ms):
            "frac": round(rate(by, ev_ms) / HBM_PEAK_GBS, 4),
            "bitwise_equal_to_write_every_round": same,
            "timing": "HIP events around whole store cycles (first round after a store "
-                     "... the storing round), no flush inside; median of 3 passes"}
-    prof = profile_cycle_ms(workload)
-    if prof is not None:
-        out["rocprof_cycle_ms_per_round"] = prof[0]
-        out["rocprof_source"] = prof[1]
-        out["events_vs_rocprof"] = round(ev_ms / prof[0], 4)
+                     "... the storing round), no flush inside; median of 3 passes, each "
+                     "from a fresh A_0 after 2 warm-up cycles"}
+    add_rocprof(out, workload, ev_ms, by)
     sh.close()
     del sh
     torch.cuda.empty_cache()
@@ -1076,9 +1097,11 @@ def main():
     # (split launch: local columns while the all-gather runs on a second
     # stream, sharded.py overlap=True).  Both schedules compute the same
     # round (A, v, m and the stop decisions bitwise; s to rounding where a
-    # piece straddles the local columns); the line's `value` is the faster
-    # of the two on this machine and the other is reported beside it
-    # (`exchange_schedule`; --overlap forces the overlapped one)
+    # piece straddles the local columns).  A selection pass times both; the
+    # line's `value` is then a FRESH pass of the faster one, and the other
+    # is reported beside it (`exchange_other_schedule`; --overlap forces the
+    # overlapped one).  Rounds 1-3 timed the plain schedule only; round 4
+    # took the faster selection timing as the value (biased up)
     overlap_leg = None
     schedule = "overlapped" if args.overlap else "plain"
     if world > 1 and not args.overlap and not args.no_overlap_leg:
@@ -1087,25 +1110,38 @@ def main():
         lam_ov, _, it_ov, _ = ov.solve(eps=1e-3, max_itr=1000, batch=1)
         ov.load(args.kind)
         el_ov, k_ov = timed_rounds(ov, args.steps, args.warmup, torch, dist, world)
-        overlap_leg = {"ms_per_iteration": round(el_ov / args.steps * 1e3, 5),
-                       "value": round(bytes_round_total * args.steps / el_ov / 1e9, 2),
-                       "round_ms_avg": round(k_ov, 5),
-                       "solve_iter_count": it_ov,
-                       "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
-        ov.close()
-        del ov
-        progress(f"overlapped-exchange leg done: {overlap_leg['ms_per_iteration']} ms per round "
-                 f"(plain {el / args.steps * 1e3:.5f})")
-        if el_ov < el and it_ov == iters:
+        progress(f"overlapped-exchange selection pass: {el_ov / args.steps * 1e3:.5f} ms per "
+                 f"round (plain {el / args.steps * 1e3:.5f})")
+        # the two timings above only SELECT the schedule; the headline is a
+        # fresh timed pass of the chosen one (taking the faster of two noisy
+        # runs as the value would bias it upward)
+        chosen_ov = el_ov < el and it_ov == iters
+        sel = {"plain_ms_per_iteration": round(el / args.steps * 1e3, 5),
+               "overlapped_ms_per_iteration": round(el_ov / args.steps * 1e3, 5),
+               "chosen": "overlapped" if chosen_ov else "plain"}
+        if chosen_ov:
             overlap_leg = {"schedule": "plain (all-gather after the round)",
-                           "ms_per_iteration": round(el / args.steps * 1e3, 5),
+                           "ms_per_iteration": sel["plain_ms_per_iteration"],
                            "value": round(value, 2), "round_ms_avg": round(fused_ms, 5),
                            "solve_iter_count": iters}
-            el, fused_ms, schedule = el_ov, k_ov, "overlapped"
-            value = bytes_round_total * args.steps / el / 1e9
-            achieved = rate(bytes_round_local, fused_ms)
+            tgt, schedule = ov, "overlapped"
         else:
-            overlap_leg["schedule"] = "overlapped (split round, all-gather on a second stream)"
+            overlap_leg = {"schedule": "overlapped (split round, all-gather on a second stream)",
+                           "ms_per_iteration": sel["overlapped_ms_per_iteration"],
+                           "value": round(bytes_round_total * args.steps / el_ov / 1e9, 2),
+                           "round_ms_avg": round(k_ov, 5), "solve_iter_count": it_ov,
+                           "eigen_val_rel_diff": abs(lam_ov - lam) / abs(lam)}
+            tgt = sh
+        tgt.load(args.kind)
+        el, fused_ms = timed_rounds(tgt, args.steps, args.warmup, torch, dist, world)
+        value = bytes_round_total * args.steps / el / 1e9
+        achieved = rate(bytes_round_local, fused_ms)
+        overlap_leg["selection_pass"] = sel
+        overlap_leg["timing"] = ("the other schedule's selection-pass timing; the headline "
+                                 "is a fresh pass of the chosen schedule")
+        ov.close()
+        del ov, tgt
+        progress(f"headline pass ({schedule}): {el / args.steps * 1e3:.5f} ms per round")
 
     use_overlap = schedule == "overlapped"
     flat_pays = dev.flat_round_pays(p.nrows, n, dt)

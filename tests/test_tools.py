@@ -132,3 +132,46 @@ def test_citation_checker_expands_ellipsis_names():
     pats = cc.cited_patterns()
     assert "r01_sweep_dir_policy_table.txt" in pats
     assert cc.uncited() == []
+
+
+def test_defer_profile_bench_leg_passes(tmp_path):
+    """tools/defer_profile.py --bench-leg: a kernel trace of bench.py's own
+    deferred leg is cut into passes at k_recip (each pass's deferred_start
+    after a fresh load), the warm-up cycles are dropped, each pass's timed
+    k_flat + k_parts time per round is taken and the block's figure is the
+    median pass - next to the leg's HIP-event passes.  The
+    leg's trailing bitwise check (2m rounds) is not a pass."""
+    m, cycles, warm = 6, 3, 2
+    rows, t = [], 0
+
+    def k(name, d):
+        nonlocal t
+        rows.append({"Kernel_Name": name, "Start_Timestamp": t, "End_Timestamp": t + d})
+        t += d + 50
+
+    pass_us = [1000, 1200, 1100]          # per-round k_flat time of each pass's timed cycles
+    for p, fl in enumerate(pass_us + [5000]):
+        k("void st::dev::k_generate<double>(double*)", 500)
+        k("void st::dev::k_recip<double>(double const*, double*, unsigned int)", 10)
+        ncyc = warm + cycles if p < 3 else 2
+        for c in range(ncyc):
+            for np_ in range(m):
+                k(_kflat(np_, np_ == m - 1), 3000 if c < warm else fl)
+                k("void st::dev::k_parts_seg<double, 16, 256>(double const*)", 100)
+    _write(tmp_path / "trace.csv", ["Kernel_Name", "Start_Timestamp", "End_Timestamp"], rows)
+    by = 7.0 / 6.0 * 8192 * 8192 * 8
+    leg = {"deferred_writes": {"configs[1] hilbert8192_f64": {
+        "stores_every": m, "cycles": cycles, "bytes_per_round": by,
+        "ms_per_iteration_passes": [0.0010, 0.0011, 0.0012]}}}
+    (tmp_path / "leg.out").write_text("noise\n@@LEG " + json.dumps(leg) + "\n")
+    out = tmp_path / "bench_leg.json"
+    subprocess.run([sys.executable, os.path.join(TOOLS, "defer_profile.py"), "--kind", "hilbert",
+                    "--trace", str(tmp_path / "trace.csv"), "--bench-leg",
+                    str(tmp_path / "leg.out"), "--json", str(out)], check=True,
+                   capture_output=True)
+    b = json.load(open(out))["blocks"]
+    assert len(b) == 1 and b[0]["workload"] == "hilbert8192_f64"
+    assert b[0]["rocprof_ms_per_round_passes"] == [0.0011, 0.0013, 0.0012]   # k_flat + k_parts
+    assert b[0]["rocprof_ms_per_round"] == 0.0012
+    assert b[0]["event_ms_per_round"] == 0.0011
+    assert b[0]["events_over_rocprof"] == round(0.0011 / 0.0012, 4)

@@ -332,6 +332,81 @@ def summarise(path, n, elem, m, workload, events=None, launches=None, block_rows
     return out
 
 
+def summarise_bench_leg(trace, leg_out, kind):
+    """--bench-leg: a rocprofv3 kernel trace of bench.py's own deferred
+    leg (`bench.py --leg deferred|weak_rank_blocks|rank_blocks`), summarised
+    the way the leg times it with HIP events: every pass
+    starts at its k_recip (deferred_start, after a fresh load), runs `warm`
+    store cycles and then the timed `cycles` x m rounds; per pass the
+    k_flat + k_parts kernel time of the timed rounds / rounds, per block the
+    median of its 3 passes beside the leg's own HIP-event passes."""
+    LEG_TAG = "@@LEG "
+    leg = None
+    for ln in open(leg_out):
+        if ln.startswith(LEG_TAG):
+            leg = json.loads(ln[len(LEG_TAG):])
+    assert leg is not None, f"no {LEG_TAG.strip()} line in {leg_out}"
+    blocks = []          # (workload, m, cycles, warm, event passes, bytes per round)
+    if "deferred_writes" in leg:
+        for name, d in leg["deferred_writes"].items():
+            wl = name.split()[-1]
+            blocks.append((wl, d["stores_every"], d["cycles"], 2, d["ms_per_iteration_passes"],
+                           d["bytes_per_round"]))
+    for key in ("weak_rank_blocks", "rank_blocks"):
+        for P, d in leg.get(key, {}).items():
+            if not P.startswith("P") or "deferred_writes" not in d:
+                continue
+            dw = d["deferred_writes"]
+            m = dw["stores_every"]
+            blocks.append((f"{kind}{d['cols']}_p{P[1:]}_f64", m, dw["cycles"], 1,
+                           dw["ms_per_iteration_passes"],
+                           (m + 1.0) / m * d["rows"] * d["cols"] * 8))
+    rows = list(csv.DictReader(open(trace)))
+    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+    dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # noqa: E731
+    segs, cur, flat = [], None, None
+    for r in rows:
+        name = r["Kernel_Name"]
+        if "k_recip<" in name:
+            cur = []
+            segs.append(cur)
+            flat = None
+        elif cur is not None and "k_flat<" in name and np_of(name) >= 0:
+            flat = dur(r)
+        elif cur is not None and flat is not None and ("k_parts<" in name
+                                                       or "k_parts_seg<" in name):
+            cur.append(flat + dur(r))
+            flat = None
+    segs = [x for x in segs if x]
+    out = {"source": "bench.py leg under rocprofv3 --kernel-trace", "trace": trace,
+           "leg_out": leg_out, "blocks": []}
+    i = 0
+    med = lambda x: sorted(x)[len(x) // 2]  # noqa: E731
+    for wl, m, cycles, warm, ev_passes, by in blocks:
+        passes = []
+        for _ in range(3):
+            while i < len(segs) and len(segs[i]) < (warm + cycles) * m:
+                i += 1            # not a timed pass (e.g. the leg's bitwise check)
+            assert i < len(segs), f"{wl}: trace ends before its 3 passes"
+            t = segs[i][warm * m:(warm + cycles) * m]
+            passes.append(sum(t) / len(t))
+            i += 1
+        rp = med(passes)
+        ev = med(ev_passes)
+        b = {"workload": wl, "m": m, "cycles": cycles, "warm_cycles": warm,
+             "rocprof_ms_per_round_passes": [round(x, 5) for x in passes],
+             "rocprof_ms_per_round": round(rp, 5),
+             "rocprof_GBs": round(by / (rp * 1e-3) / 1e9, 1),
+             "rocprof_frac": round(by / (rp * 1e-3) / 1e9 / 8000.0, 4),
+             "event_ms_per_round_passes": ev_passes, "event_ms_per_round": ev,
+             "events_over_rocprof": round(ev / rp, 4), "bytes_per_round": by}
+        out["blocks"].append(b)
+        print(f"{wl}: rocprof {rp:.5f} ms per round (passes "
+              f"{', '.join(f'{x:.5f}' for x in passes)}), HIP events {ev:.5f} "
+              f"(x{ev / rp:.4f}), {b['rocprof_frac']:.4f} of 8 TB/s")
+    return out
+
+
 def summarise_pmc(fetch, write, n, elem, m, rows=None):
     """HBM bytes per deferred k_flat launch by pending count: 2*FETCH_SIZE
     (the gfx950 wide-read correction, MI355X_MICROARCH.md §HBM) + WRITE_SIZE,
@@ -389,6 +464,8 @@ if __name__ == "__main__":
     p.add_argument("--rank-block", type=int, default=0,
                    help="rank 0's block of a P-way row partition (no exchange)")
     p.add_argument("--write")
+    p.add_argument("--bench-leg", help="with --trace: the stdout of the profiled "
+                   "`bench.py --leg ...` run; summarise its timed deferred passes")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
@@ -401,6 +478,10 @@ if __name__ == "__main__":
              run_every_ab(a) if a.every_ab else run_caps_ab(a))
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)
+    elif a.trace and a.bench_leg:
+        res = summarise_bench_leg(a.trace, a.bench_leg, a.kind)
+        if a.json:
+            json.dump(res, open(a.json, "w"), indent=1)
     elif a.trace or a.fetch:
         res = {}
         if a.trace:

@@ -24,5 +24,19 @@ rcclchar)
   # RCCL deadline behaviour on torch's bundled RCCL (a crash at exit is the finding)
   timeout -k 5 40 python3 tools/rccl_deadline_torch.py --abort 0 > $O/rcclchar_noabort.log 2>&1; echo "rcclchar_noabort rc=$?"; grep "^\[" $O/rcclchar_noabort.log
   timeout -k 5 40 python3 tools/rccl_deadline_torch.py --abort 1 > $O/rcclchar_abort.log 2>&1; echo "rcclchar_abort rc=$?"; grep "^\[" $O/rcclchar_abort.log ;;
+deferleg)
+  # the bench's own deferred legs under a kernel trace: the
+  # rocprof source bench.py quotes beside its HIP-event figure
+  EV='"every_ms":{"hilbert8192_f64":0.153,"random32768_f64":2.64,"random32768_f32":1.31}'
+  for W in "0 hilbert8192_f64" "1 random32768_f64" "2 random32768_f32"; do
+    set -- $W; I=$1; WL=$2; D=$O/deferleg_$WL; mkdir -p $D
+    run deferleg_$WL 600 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg deferred --leg-args "{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true,\"which\":$I,$EV}"
+    python3 tools/defer_profile.py --kind hilbert --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$WL.log --json $O/r05_defer_bench_$WL.json
+  done
+  for W in "weak_rank_blocks hilbert" "rank_blocks random"; do
+    set -- $W; L=$1; K=$2; D=$O/deferleg_$L; mkdir -p $D
+    run deferleg_$L 900 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg $L --leg-args "{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true}"
+    python3 tools/defer_profile.py --kind $K --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$L.log --json $O/r05_defer_bench_$L.json
+  done ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac; done
