@@ -12,6 +12,10 @@ run() { # name secs cmd...  (rc 0/1 continue; anything else ends the session)
 }
 for step in ${STEPS:-tests smoke bench}; do case $step in
 comm) run comm_tests 400 python3 -u -m pytest -x -v -s --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fullsize.py -k "comm_init or grouped_init or all_devices or config3"; tail -40 $O/comm_tests.log ;;
+bitwise)
+  # the flat launches' bitwise tests first: a failure ends the session
+  timeout -k 10 400 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "tail or 2d_grid or flat_round_vs_round or deferred_writes_bitwise or mfree_flat or split_flat" > $O/bitwise.log 2>&1; rc=$?
+  tail -3 $O/bitwise.log; [ $rc -eq 0 ] || fail bitwise $rc ;;
 tests) run pytest_gpu 900 python3 -u -m pytest -x -q -rs --timeout 300 --timeout-method thread -m gpu tests/; tail -15 $O/pytest_gpu.log ;;
 smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -3 $O/smoke.log ;;
 bench) run bench 900 python3 bench.py; tail -c 1500 $O/bench.log ;;
@@ -37,6 +41,34 @@ deferleg)
     set -- $W; L=$1; K=$2; D=$O/deferleg_$L; mkdir -p $D
     run deferleg_$L 900 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg $L --leg-args "{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true}"
     python3 tools/defer_profile.py --kind $K --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$L.log --json $O/r05_defer_bench_$L.json
+  done ;;
+tailab)
+  # ragged rows' tail workgroups: off / table / 2 / 4 / 8 row
+  # groups per workgroup of the last piece, every-round and deferred
+  for W in "11648 2" "23040 8" "4352 0"; do
+    set -- $W; N=$1; P=$2
+    run tailab_h${N}_p${P} 400 python3 tools/defer_profile.py --kind hilbert --n $N --rank-block $P --dtype f64 --tail-ab "1;0;2;4;8" --steps 100 --cycles 20 --passes 7 --ab-json $O/r05_tail_ab_h${N}_p${P}.json
+    grep median $O/tailab_h${N}_p${P}.log
+  done ;;
+loopab)
+  # the tail loop around k_flat's body against the round-4 build (ab_base)
+  # on whole-piece blocks (the headline shapes), alternating builds
+  for rep in 1 2; do for V in new base; do
+    L=eigen_value_amd/lib/libsimilarity_transform.so; [ $V = base ] && L=eigen_value_amd/lib/ab_base/libsimilarity_transform.so
+    for W in "8192 0" "16384 4" "32768 0"; do
+      set -- $W; N=$1; P=$2; K=hilbert; [ $N = 32768 ] && K=random
+      EIGEN_VALUE_LIB=$L run loopab_${V}${rep}_${N}_p${P} 300 python3 tools/defer_profile.py --kind $K --n $N --rank-block $P --dtype f64 --tail-ab "1" --steps 100 --cycles 6 --passes 5 --ab-json $O/r05_loop_ab_${V}${rep}_${N}_p${P}.json
+      grep median $O/loopab_${V}${rep}_${N}_p${P}.log | sed "s/^/$V$rep /"
+    done
+  done; done ;;
+storenp)
+  # VERDICT r04 #7, one bounded attempt: what the storing launch pays for
+  # its pending scalings - single k_flat launches (tools/bin/flat_map_sweep,
+  # built on the CPU) with the store at NP = 5 (shipped) against NP = 2,
+  # same rows / tile, 32768^2 and the P = 8 block of configs[3]
+  for SNP in 5 2; do
+    FMS_R8=1 FMS_MAX_NP=5 FMS_PT=16 FMS_STORE_NP=$SNP run storenp_$SNP 300 ./tools/bin/flat_map_sweep f64 32768 8192x65536
+    cat $O/storenp_$SNP.log
   done ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac; done
