@@ -203,11 +203,13 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     it - instead of the first RCCL call (init, or torch's broadcast of the
     id) waiting for it indefinitely.
 
-    payload_from_first: called on group rank 0 once everyone is present; its
-    bytes (or an exception's text) reach every rank, which returns them.
+    payload_from_first: called on group rank 0 once everyone is present,
+    with the ranks' host names (each rank's key holds its own); its bytes
+    (or an exception's text) reach every rank, which returns them.
     Calls are matched across ranks by order: every rank must make the same
     sequence of rendezvous calls on a group."""
     import datetime
+    import socket
 
     import torch.distributed as dist
     if timeout is None:
@@ -216,7 +218,7 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     _RDV_SEQ[0] += 1
     base = f"eigen_value_amd/rdv/{tag}/{_RDV_SEQ[0]}"
     store = _group_store(group)
-    store.set(f"{base}/here/{rank}", b"1")
+    store.set(f"{base}/here/{rank}", socket.gethostname().encode() or b"?")
     keys = [f"{base}/here/{r}" for r in range(world)]
     try:
         store.wait(keys, datetime.timedelta(seconds=timeout))
@@ -236,7 +238,8 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     key = f"{base}/payload"
     if rank == 0:
         try:
-            data = b"ok:" + bytes(payload_from_first())
+            hosts = [store.get(k).decode(errors="replace") for k in keys]
+            data = b"ok:" + bytes(payload_from_first(hosts))
         except Exception as e:  # noqa: BLE001 - reaches every rank below
             data = b"error:" + f"{type(e).__name__}: {e}".encode()
         store.set(key, data)
@@ -270,9 +273,22 @@ class RcclComm:
         rank = dist.get_rank(group)
         dev = torch.cuda.current_device() if device_index is None else device_index
 
-        def make_id():
-            uid = ctypes.create_string_buffer(128)
-            _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
+        def make_id(hosts):
+            # every rank on this host: the library's rendezvous listens on
+            # the loopback address (no interface choice involved), unless
+            # the caller chose one (ST_COMM_ADDR)
+            import os
+            import socket
+            local = all(h == socket.gethostname() for h in hosts)
+            set_lo = local and "ST_COMM_ADDR" not in os.environ
+            if set_lo:
+                os.environ["ST_COMM_ADDR"] = "127.0.0.1"
+            try:
+                uid = ctypes.create_string_buffer(128)
+                _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
+            finally:
+                if set_lo:
+                    del os.environ["ST_COMM_ADDR"]
             return uid.raw
 
         uid = rendezvous(group, timeout, payload_from_first=make_id)

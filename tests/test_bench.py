@@ -32,6 +32,16 @@ def test_committed_measurements_are_found():
     lam = bench.true_lambda(32768, "f64", 0)
     assert lam is not None and abs(lam / 16384 - 1) < 1e-3
     assert bench.true_lambda(3, "f64", 0) is None
+    # the deferred legs' rocprof sources: kernel traces of the bench's own
+    # legs (profiles/*_defer_bench_*.json), one per workload the line prices
+    for wl in ("hilbert8192_f64", "random32768_f64", "random32768_f32", "hilbert11648_p2_f64",
+               "hilbert16384_p4_f64", "hilbert23040_p8_f64", "random65536_p8_f64"):
+        pr = bench.profile_cycle_ms(wl)
+        assert pr is not None and pr[0] > 0 and "_defer_bench_" in pr[1], wl
+    out = {}
+    bench.add_rocprof(out, "hilbert8192_f64", 0.1, 7.0 / 6.0 * 8192 ** 2 * 8)
+    assert out["events_vs_rocprof"] == round(0.1 / out["rocprof_ms_per_round"], 4)
+    assert 0 < out["rocprof_frac"] < 1
 
 
 @pytest.mark.gpu

@@ -612,14 +612,15 @@ def _rdv_worker(rank, world, port, stall_rank, outdir):
             t0 = time.time()
             try:
                 res["payload"] = sharded.rendezvous(
-                    None, 2.0, payload_from_first=lambda: b"id-bytes").decode()
+                    None, 2.0,
+                    payload_from_first=lambda hosts: f"id-bytes {len(hosts)}".encode()).decode()
             except sharded.PeerMissingError as e:
                 res.update(missing=e.missing, msg=str(e))
             res["el"] = time.time() - t0
             # a second rendezvous on the same group (the next communicator)
             # is matched by order and does not see the first one's keys
             if stall_rank < 0:
-                def boom():
+                def boom(hosts):
                     raise RuntimeError("no id today")
                 try:
                     sharded.rendezvous(None, 5.0, payload_from_first=boom)
@@ -646,7 +647,7 @@ def test_rendezvous_names_the_missing_rank(tmp_path, stall_rank):
         if r == stall_rank:
             continue
         if stall_rank < 0:
-            assert res["payload"] == "id-bytes" and res["el"] < 5.0
+            assert res["payload"] == "id-bytes 3" and res["el"] < 5.0
             assert "group rank 0 failed: RuntimeError: no id today" in res["second"]
         else:
             assert res["missing"] == [1], res
