@@ -474,7 +474,8 @@ def profile_cycle_ms(workload: str):
     leg (profiles/*_defer_bench_*.json, tools/defer_profile.py --bench-leg:
     k_flat + k_parts of the timed cycles, median pass of 3, each from a
     fresh A_0 - the procedure the leg times with HIP events).  The latest
-    round's file wins; (ms per round, path) or None."""
+    round's file wins; (ms per round, path, the trace's own slowdown of the
+    leg's HIP-event time or None) or None."""
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(HERE, "profiles", "*_defer_bench_*.json"))):
@@ -484,7 +485,8 @@ def profile_cycle_ms(workload: str):
             continue
         for blk in d.get("blocks", []):
             if blk.get("workload") == workload:
-                best = (blk["rocprof_ms_per_round"], os.path.relpath(f, HERE))
+                best = (blk["rocprof_ms_per_round"], os.path.relpath(f, HERE),
+                        blk.get("trace_slowdown"))
     return best
 
 
@@ -497,6 +499,12 @@ def add_rocprof(out: dict, workload: str, ev_ms: float, by: float) -> None:
         out["rocprof_frac"] = round(rate(by, prof[0]) / HBM_PEAK_GBS, 4)
         out["rocprof_source"] = prof[1]
         out["events_vs_rocprof"] = round(ev_ms / prof[0], 4)
+        if prof[2]:
+            # kernel tracing slows short rounds itself (a completion signal
+            # and timestamps per dispatch): the same leg untraced on the
+            # profiling box, so the two untraced figures compare directly
+            out["rocprof_trace_slowdown"] = prof[2]
+            out["events_vs_rocprof_untraced"] = round(ev_ms * prof[2] / prof[0], 4)
 
 
 # ---------------------------------------------------------------------------

@@ -332,21 +332,16 @@ def summarise(path, n, elem, m, workload, events=None, launches=None, block_rows
     return out
 
 
-def summarise_bench_leg(trace, leg_out, kind):
-    """--bench-leg: a rocprofv3 kernel trace of bench.py's own deferred
-    leg (`bench.py --leg deferred|weak_rank_blocks|rank_blocks`), summarised
-    the way the leg times it with HIP events (VERDICT r04 #4): every pass
-    starts at its k_recip (deferred_start, after a fresh load), runs `warm`
-    store cycles and then the timed `cycles` x m rounds; per pass the
-    k_flat + k_parts kernel time of the timed rounds / rounds, per block the
-    median of its 3 passes beside the leg's own HIP-event passes."""
+def leg_blocks(leg_out, kind):
+    """(workload, m, cycles, warm, HIP-event passes, bytes per round) of
+    every deferred block in a `bench.py --leg ...` stdout file."""
     LEG_TAG = "@@LEG "
     leg = None
     for ln in open(leg_out):
         if ln.startswith(LEG_TAG):
             leg = json.loads(ln[len(LEG_TAG):])
     assert leg is not None, f"no {LEG_TAG.strip()} line in {leg_out}"
-    blocks = []          # (workload, m, cycles, warm, event passes, bytes per round)
+    blocks = []
     if "deferred_writes" in leg:
         for name, d in leg["deferred_writes"].items():
             wl = name.split()[-1]
@@ -361,6 +356,23 @@ def summarise_bench_leg(trace, leg_out, kind):
             blocks.append((f"{kind}{d['cols']}_p{P[1:]}_f64", m, dw["cycles"], 1,
                            dw["ms_per_iteration_passes"],
                            (m + 1.0) / m * d["rows"] * d["cols"] * 8))
+    return blocks
+
+
+def summarise_bench_leg(trace, leg_out, kind, plain_out=None):
+    """--bench-leg: a rocprofv3 kernel trace of bench.py's own deferred
+    leg (`bench.py --leg deferred|weak_rank_blocks|rank_blocks`), summarised
+    the way the leg times it with HIP events (VERDICT r04 #4): every pass
+    starts at its k_recip (deferred_start, after a fresh load), runs `warm`
+    store cycles and then the timed `cycles` x m rounds; per pass the
+    k_flat + k_parts kernel time of the timed rounds / rounds, per block the
+    median of its 3 passes beside the leg's own HIP-event passes.
+    plain_out: the same leg run WITHOUT the profiler on the same box; its
+    HIP-event medians give the trace's own slowdown (kernel tracing adds a
+    completion signal and timestamps to every dispatch: ~2 % on rounds of
+    0.1 ms, nothing on rounds of 1 ms and more)."""
+    blocks = leg_blocks(leg_out, kind)
+    plain = {b[0]: b[4] for b in leg_blocks(plain_out, kind)} if plain_out else {}
     rows = list(csv.DictReader(open(trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     dur = lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-6  # noqa: E731
@@ -400,6 +412,11 @@ def summarise_bench_leg(trace, leg_out, kind):
              "rocprof_frac": round(by / (rp * 1e-3) / 1e9 / 8000.0, 4),
              "event_ms_per_round_passes": ev_passes, "event_ms_per_round": ev,
              "events_over_rocprof": round(ev / rp, 4), "bytes_per_round": by}
+        if wl in plain:
+            pe = med(plain[wl])
+            b["event_ms_per_round_untraced"] = pe
+            b["event_ms_per_round_untraced_passes"] = plain[wl]
+            b["trace_slowdown"] = round(ev / pe, 4)
         out["blocks"].append(b)
         print(f"{wl}: rocprof {rp:.5f} ms per round (passes "
               f"{', '.join(f'{x:.5f}' for x in passes)}), HIP events {ev:.5f} "
@@ -466,6 +483,8 @@ if __name__ == "__main__":
     p.add_argument("--write")
     p.add_argument("--bench-leg", help="with --trace: the stdout of the profiled "
                    "`bench.py --leg ...` run; summarise its timed deferred passes")
+    p.add_argument("--bench-leg-plain", help="with --bench-leg: the stdout of the same leg "
+                   "run without the profiler (the trace's own slowdown)")
     a = p.parse_args()
     elem = 8 if a.dtype == "f64" else 4
     m = rounds_per_store(a.n, elem, a.dtype == "f64")
@@ -479,7 +498,7 @@ if __name__ == "__main__":
         if a.ab_json:
             json.dump(r, open(a.ab_json, "w"), indent=1)
     elif a.trace and a.bench_leg:
-        res = summarise_bench_leg(a.trace, a.bench_leg, a.kind)
+        res = summarise_bench_leg(a.trace, a.bench_leg, a.kind, a.bench_leg_plain)
         if a.json:
             json.dump(res, open(a.json, "w"), indent=1)
     elif a.trace or a.fetch:

@@ -34,13 +34,17 @@ deferleg)
   EV='"every_ms":{"hilbert8192_f64":0.153,"random32768_f64":2.64,"random32768_f32":1.31}'
   for W in "0 hilbert8192_f64" "1 random32768_f64" "2 random32768_f32"; do
     set -- $W; I=$1; WL=$2; D=$O/deferleg_$WL; mkdir -p $D
-    run deferleg_$WL 600 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg deferred --leg-args "{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true,\"which\":$I,$EV}"
-    python3 tools/defer_profile.py --kind hilbert --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$WL.log --json $O/r05_defer_bench_$WL.json
+    A="{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true,\"which\":$I,$EV}"
+    run deferleg_$WL 600 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg deferred --leg-args "$A"
+    run deferplain_$WL 600 python3 bench.py --leg deferred --leg-args "$A"
+    python3 tools/defer_profile.py --kind hilbert --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$WL.log --bench-leg-plain $O/deferplain_$WL.log --json $O/r05_defer_bench_$WL.json
   done
   for W in "weak_rank_blocks hilbert" "rank_blocks random"; do
     set -- $W; L=$1; K=$2; D=$O/deferleg_$L; mkdir -p $D
-    run deferleg_$L 900 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg $L --leg-args "{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true}"
-    python3 tools/defer_profile.py --kind $K --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$L.log --json $O/r05_defer_bench_$L.json
+    A="{\"device\":0,\"steps\":200,\"warmup\":10,\"kind\":\"hilbert\",\"n\":8192,\"dtype\":\"f64\",\"representative\":true}"
+    run deferleg_$L 900 rocprofv3 --kernel-trace --output-format csv -d $D -o run -- python3 bench.py --leg $L --leg-args "$A"
+    run deferplain_$L 900 python3 bench.py --leg $L --leg-args "$A"
+    python3 tools/defer_profile.py --kind $K --trace $D/run_kernel_trace.csv --bench-leg $O/deferleg_$L.log --bench-leg-plain $O/deferplain_$L.log --json $O/r05_defer_bench_$L.json
   done ;;
 tailab)
   # ragged rows' tail workgroups: off / table / 2 / 4 / 8 row
@@ -70,5 +74,10 @@ storenp)
     FMS_R8=1 FMS_MAX_NP=5 FMS_PT=16 FMS_STORE_NP=$SNP run storenp_$SNP 300 ./tools/bin/flat_map_sweep f64 32768 8192x65536
     cat $O/storenp_$SNP.log
   done ;;
+torchrun8)
+  # the driver's N > 1 launch line, rehearsed: torch.distributed.run with 8
+  # ranks, all on cuda:0 over gloo (--one-gpu: plumbing, not scaling data)
+  run torchrun8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 8 --steps 5 --warmup 1 --backend gloo --one-gpu
+  grep -v "^\[W\|socket.cpp\|amdgpu.ids" $O/torchrun8.log | tail -c 3000 ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac; done
