@@ -451,9 +451,13 @@ rdv_make_id(char* out)
   RdvId id;
   std::memset(&id, 0, sizeof id);
   std::memcpy(id.magic, kMagic, sizeof kMagic);
-  std::random_device rd;
-  id.nonce = ((uint64_t)rd() << 32) ^ rd() ^ ((uint64_t)getpid() << 16) ^
-             (uint64_t)Clock::now().time_since_epoch().count();
+  id.nonce = ((uint64_t)getpid() << 40) ^
+             (uint64_t)Clock::now().time_since_epoch().count() ^ (uint64_t)fd;
+  try {
+    std::random_device rd;
+    id.nonce ^= ((uint64_t)rd() << 32) ^ rd();
+  } catch (...) { // no entropy source: pid, time and fd still differ per id
+  }
   id.addr = advertised_addr();
   id.port = sa.sin_port;
   host_name(id.host, sizeof id.host);

@@ -177,7 +177,7 @@ class PeerMissingError(_lib.EigenValueError):
         self.missing = list(missing)
 
 
-_RDV_SEQ = [0]
+_RDV_SEQ: dict = {}    # (tag, group's global ranks) -> rendezvous calls made on it
 
 
 def _group_store(group):
@@ -206,8 +206,8 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     payload_from_first: called on group rank 0 once everyone is present,
     with the ranks' host names (each rank's key holds its own); its bytes
     (or an exception's text) reach every rank, which returns them.
-    Calls are matched across ranks by order: every rank must make the same
-    sequence of rendezvous calls on a group."""
+    Calls are matched across ranks by order within a group: every rank of
+    a group must make the same sequence of rendezvous calls on it."""
     import datetime
     import socket
 
@@ -215,8 +215,10 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     if timeout is None:
         timeout = _lib.load().st_get_comm_timeout()
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    _RDV_SEQ[0] += 1
-    base = f"eigen_value_amd/rdv/{tag}/{_RDV_SEQ[0]}"
+    gkey = (tag, tuple(dist.get_global_rank(group, r) for r in range(world))
+            if group is not None else None)
+    _RDV_SEQ[gkey] = seq = _RDV_SEQ.get(gkey, 0) + 1     # matched per group, by order
+    base = f"eigen_value_amd/rdv/{tag}/{seq}"
     store = _group_store(group)
     store.set(f"{base}/here/{rank}", socket.gethostname().encode() or b"?")
     keys = [f"{base}/here/{r}" for r in range(world)]
