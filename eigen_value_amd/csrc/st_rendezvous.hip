@@ -360,7 +360,8 @@ peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
       ::st::set_error("st_comm_init: RCCL rank %d of %d could not reach the id's "
                       "host at %s within %.1f s (ST_COMM_TIMEOUT_S / "
                       "st_set_comm_timeout): the rank that made the id did not "
-                      "reach st_comm_init; no rank entered RCCL",
+                      "reach st_comm_init, or gave up on a missing rank before "
+                      "this one arrived; no rank entered RCCL",
                       rank, nranks, where.c_str(), seconds_since(t0));
       return -1;
     }
