@@ -604,6 +604,7 @@ def _rdv_worker(rank, world, port, stall_rank, outdir):
     from eigen_value_amd import sharded
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.barrier()            # every rank's mesh is up before one of them moves on
     res = {"rank": rank}
     try:
         if rank == stall_rank:
@@ -629,6 +630,7 @@ def _rdv_worker(rank, world, port, stall_rank, outdir):
         import json
         with open(os.path.join(outdir, f"rdv{rank}.json"), "w") as f:
             json.dump(res, f)
+        dist.barrier()        # rank 0 hosts the store: nobody leaves before all are done
     finally:
         dist.destroy_process_group()
 
@@ -659,6 +661,7 @@ def _agree_missing_worker(rank, world, port, outdir):
     from eigen_value_amd import sharded
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    dist.barrier()
     try:
         def factory():
             # as RcclComm reports a rank absent from st_comm_init's rendezvous
@@ -671,6 +674,7 @@ def _agree_missing_worker(rank, world, port, outdir):
         except sharded.PeerMissingError:
             out = "raised"
         open(os.path.join(outdir, f"m{rank}"), "w").write(out)
+        dist.barrier()
     finally:
         dist.destroy_process_group()
 
