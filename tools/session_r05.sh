@@ -79,5 +79,19 @@ torchrun8)
   # ranks, all on cuda:0 over gloo (--one-gpu: plumbing, not scaling data)
   run torchrun8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 8 --steps 5 --warmup 1 --backend gloo --one-gpu
   grep -v "^\[W\|socket.cpp\|amdgpu.ids" $O/torchrun8.log | tail -c 3000 ;;
+fuzz) run fuzz_parity 900 python3 -u tools/fuzz_parity.py --cases 300 --seed 20261105 --json $O/r05_fuzz_parity.json; tail -3 $O/fuzz_parity.log ;;
+pmc)
+  # HBM bytes of the headline launches (separate FETCH_SIZE / WRITE_SIZE
+  # passes, tools/pmc_traffic.py applies the gfx950 x2 FETCH correction)
+  for W in "hilbert 8192 f64 8" "random 32768 f64 8" "random 32768 f32 4"; do
+    set -- $W; K=$1; N=$2; DT=$3; E=$4; D=$O/${K}${N}_${DT}; mkdir -p $D
+    X="--kind $K --n $N --dtype $DT --no-cpu --no-north-star --no-headline"
+    run prof_${K}${N}_${DT} 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 bench.py $X
+    run pmcf_${K}${N}_${DT} 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/pmc_fetch -o run -- python3 bench.py $X --steps 20 --warmup 2
+    run pmcw_${K}${N}_${DT} 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/pmc_write -o run -- python3 bench.py $X --steps 20 --warmup 2
+    T=double; [ $DT = f32 ] && T=float
+    python3 tools/pmc_traffic.py --workload ${K}${N}_${DT} --n $N --elem $E --dtype $T --fetch $D/pmc_fetch/run_counter_collection.csv --write $D/pmc_write/run_counter_collection.csv --trace $D/prof/run_kernel_trace.csv --out $O/r05_${K}${N}_${DT}_pmc.json
+    cp $D/prof/run_kernel_stats.csv $O/r05_${K}${N}_${DT}_kernel_stats.csv
+  done ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac; done
