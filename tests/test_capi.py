@@ -346,6 +346,59 @@ def test_comm_rendezvous_peer_names_an_absent_host():
     assert "no word from the id's host" in lines["ERR"], lines["ERR"]
 
 
+_JOIN = r"""
+import ctypes, sys, time
+sys.path.insert(0, sys.argv[1])
+from eigen_value_amd import _lib
+L = _lib.load()
+L.st_set_comm_timeout(20.0)
+rank, nranks = int(sys.argv[3]), int(sys.argv[4])
+c = ctypes.c_void_p()
+t0 = time.time()
+rc = L.st_comm_init(ctypes.byref(c), nranks, rank, bytes.fromhex(sys.argv[2]), 0)
+print("RC", rc, "EL", round(time.time() - t0, 2))
+print("ERR", _lib.last_error(), flush=True)
+"""
+
+
+def test_comm_rendezvous_eight_processes_without_a_device():
+    """The driver's 8-GPU shape of st_comm_init's rendezvous, on CPU: this
+    process makes the id and joins as rank 0 while seven other processes
+    join as ranks 1..7 (in any order).  Every rank gets past the presence
+    check together - on a box without a device the id's host then cannot
+    make the RCCL id, and all eight report exactly that, promptly (never a
+    missing rank, never a hang)."""
+    import sys
+    import time
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id(uid) == 0
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    procs = [subprocess.Popen([sys.executable, "-c", _JOIN, repo, uid.raw.hex(), str(r), "8"],
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for r in (7, 3, 1, 5, 2, 6, 4)]
+    old = L.st_set_comm_timeout(20.0)
+    try:
+        comm = ctypes.c_void_p()
+        t0 = time.time()
+        rc0 = L.st_comm_init(ctypes.byref(comm), 8, 0, uid.raw, 0)
+        err0, el0 = _lib.last_error(), time.time() - t0
+    finally:
+        L.st_set_comm_timeout(old)
+    outs = [p.communicate(timeout=60) for p in procs]
+    if rc0 == 0:                               # a box with a device: RCCL ran
+        L.st_comm_destroy(comm)
+    else:
+        assert "could not make the RCCL id" in err0, err0
+    assert el0 < 15.0
+    for p, (so, se) in zip(procs, outs):
+        assert p.returncode == 0, se[-2000:]
+        lines = dict(ln.split(" ", 1) for ln in so.splitlines() if ln[:3] in ("RC ", "ERR"))
+        assert "did not reach" not in lines["ERR"] and "no word" not in lines["ERR"], lines
+        if rc0 != 0:
+            assert "could not make the RCCL id" in lines["ERR"], lines
+
+
 def test_rccl_version_is_reported():
     """st_rccl_version / _lib.rccl_info / st_version name the RCCL the
     library's calls bind to: X.Y.Z and the file holding the
