@@ -246,7 +246,13 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
             data = b"error:" + f"{type(e).__name__}: {e}".encode()
         store.set(key, data)
     else:
-        store.wait([key], datetime.timedelta(seconds=timeout))
+        try:
+            store.wait([key], datetime.timedelta(seconds=timeout))
+        except Exception as e:  # noqa: BLE001 - rank 0 stopped after arriving
+            raise PeerMissingError(
+                f"group rank 0 of {world} arrived but did not hand over the communicator id "
+                f"within {timeout:.1f} s; this is rank {rank}; no rank entered RCCL",
+                [0]) from e
         data = store.get(key)
     if data.startswith(b"error:"):
         raise _lib.EigenValueError(f"group rank 0 failed: {data[6:].decode(errors='replace')}")
