@@ -6,10 +6,14 @@
  * with good and bad arguments (the drop-in pair with a NULL queue, the
  * step kernels' argument checks, the policy query over every form and size
  * class, the tuning setters and their range checks, the communicator calls'
- * argument errors, the deadline setter), so the host-side parsing, error
- * formatting (eigen_last_error) and table lookups run under the sanitizers.
+ * argument errors, the deadline setter, st_comm_init's pre-RCCL rendezvous
+ * - a missing rank, and three ranks as threads of this process - and the
+ * RCCL version query), so the host-side parsing, error formatting
+ * (eigen_last_error), table lookups and socket code run under the
+ * sanitizers.
  * Exit 0 = clean.
  */
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
@@ -17,6 +21,27 @@
 #include "similarity_transform.h"
 
 static int fails = 0;
+
+/* three ranks of one rendezvous as threads: joined[r] = 0 (RCCL joined, a
+   device) or 1 (the rendezvous passed, the RCCL id could not be made), 2 =
+   anything else */
+static char rdv_id[ST_COMM_ID_BYTES];
+static int joined[3] = { 2, 2, 2 };
+
+static void*
+join_rank(void* arg)
+{
+  const int r = *(const int*)arg;
+  void* c = NULL;
+  if (st_comm_init(&c, 3, r, rdv_id, 0) == 0) {
+    joined[r] = 0;
+    st_comm_destroy(c);
+  } else if (strstr(eigen_last_error(), "could not make the RCCL id") ||
+             strstr(eigen_last_error(), "ncclCommInitRankConfig")) {
+    joined[r] = 1;
+  }
+  return NULL;
+}
 #define CHECK(c)                                                                 \
   do {                                                                           \
     if (!(c)) {                                                                  \
@@ -84,6 +109,33 @@ main(void)
   CHECK(st_allgather_f64(NULL, buf, buf, 1, NULL) < 0);
   const double t0 = st_set_comm_timeout(0.0);
   CHECK(st_set_comm_timeout(2.5) == t0 && st_set_comm_timeout(0.0) == 2.5);
+
+  /* st_comm_init's rendezvous (st_rendezvous.hip): a foreign id, rank 0 of
+     2 alone (missing rank named after the 1 s deadline, no RCCL state),
+     three ranks as threads (the host is whichever claims the listener;
+     without a device they all report the RCCL id failure) */
+  memset(id, 1, sizeof id);
+  CHECK(st_comm_init(&comm, 2, 0, id, 0) < 0 &&
+        strstr(eigen_last_error(), "not made by st_comm_unique_id") != NULL);
+  st_set_comm_timeout(1.0);
+  CHECK(st_get_comm_timeout() == 1.0);
+  CHECK(st_comm_unique_id(rdv_id) == 0);
+  CHECK(st_comm_init(&comm, 2, 0, rdv_id, 0) < 0 &&
+        strstr(eigen_last_error(), "rank 1 of 2 did not reach st_comm_init") != NULL);
+  CHECK(st_comm_unique_id(rdv_id) == 0);
+  pthread_t th[3];
+  int ranks[3] = { 2, 0, 1 };
+  for (int i = 0; i < 3; i++)
+    pthread_create(&th[i], NULL, join_rank, &ranks[i]);
+  for (int i = 0; i < 3; i++)
+    pthread_join(th[i], NULL);
+  for (int i = 0; i < 3; i++)
+    CHECK(joined[i] == 0 || joined[i] == 1);
+  st_set_comm_timeout(0.0);
+  int vcode = 0;
+  char vpath[512];
+  CHECK(st_rccl_version(&vcode, vpath, (int)sizeof vpath) == 0 && vcode >= 22000 &&
+        strstr(vpath, "librccl") != NULL);
 
   /* with a device: the real solve paths' host code (drop-in fp32 on a
      k_round block, fp64 on a flat block with deferred writes, the native

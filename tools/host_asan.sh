@@ -12,16 +12,16 @@ if [ "${1:-run}" = build ]; then
   mkdir -p $D
   FL="--offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off -I$ROOT/include -I$ROOT/eigen_value_amd/csrc"
   SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
-  for f in st_kernels st_solve st_multi; do
+  for f in st_kernels st_solve st_multi st_rendezvous; do
     /opt/rocm/bin/hipcc $FL $SAN -c $ROOT/eigen_value_amd/csrc/$f.hip -o $D/$f.o &
   done
   wait
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC $SAN -o $D/libsimilarity_transform.so \
-    $D/st_kernels.o $D/st_solve.o $D/st_multi.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+    $D/st_kernels.o $D/st_solve.o $D/st_multi.o $D/st_rendezvous.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   rm -f $D/*.o
   /opt/rocm/lib/llvm/bin/clang -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer \
     -I$ROOT/include $ROOT/tests/cpp/capi_sanitize.c -L$D -lsimilarity_transform \
-    -Wl,-rpath,'$ORIGIN' -o $D/capi_sanitize
+    -Wl,-rpath,'$ORIGIN' -lpthread -o $D/capi_sanitize
   echo "built $D/capi_sanitize"
 else
   # verify_asan_link_order=0: the environment may preload a library first;
