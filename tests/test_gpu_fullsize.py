@@ -212,12 +212,13 @@ def test_library_comm_all_devices(tmp_path, orc, world):
         sk.bind(("127.0.0.1", 0))
         port = sk.getsockname()[1]
     mp.spawn(_comm_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    refs = [orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL,
+                                     nthreads=HOST_THREADS) for n in (3001, 9216)]
     for r in range(world):
         got = np.load(tmp_path / f"r{r}.npy")
         assert tuple(int(x) for x in got[:3]) == (world, r, r)
         for j, n in enumerate((3001, 9216)):
-            ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL,
-                                           nthreads=HOST_THREADS)
+            ref = refs[j]
             lam, it, rounds = got[3 + 3 * j:6 + 3 * j]
             assert int(it) == ref.iter_count and int(rounds) == ref.rounds_evaluated
             assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
