@@ -26,7 +26,6 @@
 
 #include <arpa/inet.h>
 #include <errno.h>
-#include <fcntl.h>
 #include <ifaddrs.h>
 #include <net/if.h>
 #include <netinet/in.h>
@@ -171,7 +170,7 @@ read_all(int fd, void* buf, size_t len, Clock::time_point until)
   char* p = static_cast<char*>(buf);
   while (len) {
     const auto left =
-      std::chrono::duration_cast<std::chrono::milliseconds>(until - Clock::now())
+      std::chrono::ceil<std::chrono::milliseconds>(until - Clock::now())
         .count();
     if (left <= 0 || !wait_fd(fd, POLLIN, (int)std::min<long long>(left, 200)))
     {
@@ -260,12 +259,11 @@ host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
   const auto until = t0 + std::chrono::duration_cast<Clock::duration>(
                             std::chrono::duration<double>(limit));
   std::vector<int> fds(nranks, -1); // fds[r]: rank r's connection
-  std::vector<Hello> who(nranks);
   int present = 1;
   std::string fail;
   while (present < nranks && fail.empty()) {
     const auto left =
-      std::chrono::duration_cast<std::chrono::milliseconds>(until - Clock::now())
+      std::chrono::ceil<std::chrono::milliseconds>(until - Clock::now())
         .count();
     if (left <= 0)
       break;
@@ -302,7 +300,6 @@ host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
       break;
     }
     fds[h.rank] = c;
-    who[h.rank] = h;
     present++;
   }
   if (fail.empty() && present < nranks) {

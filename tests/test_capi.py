@@ -289,7 +289,7 @@ def test_comm_rendezvous_names_the_missing_ranks_without_a_device():
         assert L.st_comm_init(ctypes.byref(comm), 3, 0, uid.raw, 0) < 0
         el = time.time() - t0
         err = _lib.last_error()
-        assert 2.0 <= el < 8.0, el
+        assert 1.9 <= el < 8.0, el
         assert "ranks 1, 2 of 3 did not reach st_comm_init" in err, err
         assert "no rank entered RCCL" in err and comm.value is None
         # all present: the id's host is whichever thread claims the listener

@@ -654,7 +654,7 @@ def test_rendezvous_names_the_missing_rank(tmp_path, stall_rank):
         else:
             assert res["missing"] == [1], res
             assert "group rank 1 of 3 did not reach the communicator rendezvous" in res["msg"]
-            assert 2.0 <= res["el"] < 5.5, res
+            assert 1.9 <= res["el"] < 5.5, res
 
 
 def _agree_missing_worker(rank, world, port, outdir):
