@@ -218,6 +218,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_every_cache_class.restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32
+    L.st_comm_unique_id_addr.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+    L.st_comm_unique_id_addr.restype = i32
     L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]
     L.st_comm_init.restype = i32
     L.st_comm_destroy.argtypes = [P]

@@ -760,6 +760,14 @@ st_comm_unique_id(char* id_out /* ST_COMM_ID_BYTES */)
 }
 
 int
+st_comm_unique_id_addr(char* id_out, const char* addr)
+{
+  st::clear_error();
+  ST_REQUIRE(id_out, "st_comm_unique_id_addr: null output");
+  return st::rdv_make_id(id_out, addr);
+}
+
+int
 st_comm_init(void** comm, int nranks, int rank, const char* id_in, int device)
 {
   st::clear_error();

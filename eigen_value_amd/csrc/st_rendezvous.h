@@ -8,8 +8,9 @@ namespace st {
 constexpr int kRdvIdBytes = 128;      // st_comm_unique_id's id
 constexpr int kRdvPayloadBytes = 128; // what the host hands every rank (the RCCL id)
 
-// A new rendezvous id (listener opened in this process); 0 or -1.
-int rdv_make_id(char* out);
+// A new rendezvous id (listener opened in this process) advertising `addr`
+// (dotted IPv4; NULL = ST_COMM_ADDR / the interface choice); 0 or -1.
+int rdv_make_id(char* out, const char* addr = nullptr);
 
 // Join the rendezvous of `id` as `rank` of `nranks`.  The first call in the
 // process that made the id hosts it: once every rank is present it calls

@@ -113,12 +113,18 @@ ip_str(uint32_t addr_be)
   return b;
 }
 
-// The address peers connect to: ST_COMM_ADDR, else the first IPv4 address
+// The address peers connect to: the caller's (st_comm_unique_id_addr), else
+// ST_COMM_ADDR, else the first IPv4 address
 // of NCCL_SOCKET_IFNAME's interface (a plain prefix), else of the first up
 // non-loopback interface (RCCL's own bootstrap choice), else 127.0.0.1.
 uint32_t
-advertised_addr()
+advertised_addr(const char* addr)
 {
+  if (addr) {
+    in_addr a;
+    if (inet_pton(AF_INET, addr, &a) == 1)
+      return a.s_addr;
+  }
   if (const char* e = std::getenv("ST_COMM_ADDR")) {
     in_addr a;
     if (inet_pton(AF_INET, e, &a) == 1)
@@ -429,7 +435,7 @@ peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
 } // namespace
 
 int
-rdv_make_id(char* out)
+rdv_make_id(char* out, const char* addr)
 {
   const int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
   ST_REQUIRE(fd >= 0, "st_comm_unique_id: socket: %s", std::strerror(errno));
@@ -456,7 +462,15 @@ rdv_make_id(char* out)
     id.nonce ^= ((uint64_t)rd() << 32) ^ rd();
   } catch (...) { // no entropy source: pid, time and fd still differ per id
   }
-  id.addr = advertised_addr();
+  if (addr) {
+    in_addr a;
+    if (inet_pton(AF_INET, addr, &a) != 1) {
+      close(fd);
+      ::st::set_error("st_comm_unique_id_addr: %s is not an IPv4 address", addr);
+      return -1;
+    }
+  }
+  id.addr = advertised_addr(addr);
   id.port = sa.sin_port;
   host_name(id.host, sizeof id.host);
   {

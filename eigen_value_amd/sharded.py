@@ -282,21 +282,15 @@ class RcclComm:
         dev = torch.cuda.current_device() if device_index is None else device_index
 
         def make_id(hosts):
-            # every rank on this host: the library's rendezvous listens on
+            # every rank on this host: the library's rendezvous advertises
             # the loopback address (no interface choice involved), unless
             # the caller chose one (ST_COMM_ADDR)
             import os
             import socket
             local = all(h == socket.gethostname() for h in hosts)
-            set_lo = local and "ST_COMM_ADDR" not in os.environ
-            if set_lo:
-                os.environ["ST_COMM_ADDR"] = "127.0.0.1"
-            try:
-                uid = ctypes.create_string_buffer(128)
-                _lib.check(self.L.st_comm_unique_id(uid), "st_comm_unique_id")
-            finally:
-                if set_lo:
-                    del os.environ["ST_COMM_ADDR"]
+            addr = b"127.0.0.1" if local and "ST_COMM_ADDR" not in os.environ else None
+            uid = ctypes.create_string_buffer(128)
+            _lib.check(self.L.st_comm_unique_id_addr(uid, addr), "st_comm_unique_id_addr")
             return uid.raw
 
         uid = rendezvous(group, timeout, payload_from_first=make_id)

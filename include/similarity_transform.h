@@ -209,6 +209,9 @@ int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
  * says to end the process with _exit: a peer died after the rendezvous). */
 #define ST_COMM_ID_BYTES 128
 int st_comm_unique_id(char* id_out);
+/* The same, advertising `addr` (dotted IPv4, e.g. "127.0.0.1" when every
+ * rank runs on this host; NULL = the choice above). */
+int st_comm_unique_id_addr(char* id_out, const char* addr);
 int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
                  int device);
 int st_comm_destroy(void* comm);

@@ -260,6 +260,22 @@ def test_comm_calls_reject_bad_arguments_without_a_device():
     assert L.st_allgather_f64(None, buf, buf, 1, None) < 0
 
 
+def test_comm_unique_id_addr():
+    """st_comm_unique_id_addr advertises the caller's IPv4 address (the
+    Python driver passes 127.0.0.1 for a single-host group instead of
+    setting ST_COMM_ADDR in a running process); a malformed one is refused."""
+    import socket
+    import struct
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id_addr(uid, b"127.0.0.1") == 0
+    assert uid.raw[:7] == b"st-rdv1"
+    assert socket.inet_ntoa(uid.raw[16:20]) == "127.0.0.1"        # RdvId.addr
+    assert struct.unpack(">H", uid.raw[20:22])[0] > 0               # RdvId.port
+    assert L.st_comm_unique_id_addr(uid, b"not-an-address") < 0
+    assert "not an IPv4 address" in _lib.last_error()
+
+
 def test_comm_init_rejects_a_foreign_id():
     """An id that st_comm_unique_id did not make (e.g. raw RCCL id bytes) is
     refused before any socket, HIP or RCCL call."""
