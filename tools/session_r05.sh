@@ -79,6 +79,7 @@ torchrun8)
   # ranks, all on cuda:0 over gloo (--one-gpu: plumbing, not scaling data)
   run torchrun8 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29515 bench.py --gpus 8 --steps 5 --warmup 1 --backend gloo --one-gpu
   grep -v "^\[W\|socket.cpp\|amdgpu.ids" $O/torchrun8.log | tail -c 3000 ;;
+fuzzbig) run fuzz_parity_big 1100 python3 -u tools/fuzz_parity.py --cases 1500 --seed 5052026 --json $O/r05_fuzz_parity_1500.json; tail -2 $O/fuzz_parity_big.log ;;
 fuzz) run fuzz_parity 900 python3 -u tools/fuzz_parity.py --cases 300 --seed 20261105 --json $O/r05_fuzz_parity.json; tail -3 $O/fuzz_parity.log ;;
 pmc)
   # HBM bytes of the headline launches (separate FETCH_SIZE / WRITE_SIZE
