@@ -275,9 +275,9 @@ host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
       break;
     if (!wait_fd(lfd, POLLIN, (int)std::min<long long>(left, 200)))
       continue;
-    const int c = accept(lfd, nullptr, nullptr);
+    const int c = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC); // blocking
     if (c < 0)
-      continue;
+      continue; // EAGAIN (reset in between) or EINTR: poll again
     int one = 1;
     setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
     Hello h;
@@ -437,7 +437,9 @@ peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
 int
 rdv_make_id(char* out, const char* addr)
 {
-  const int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC, 0);
+  // non-blocking: accept after poll must not block on a connection that
+  // was reset in between (host_join polls, then accepts)
+  const int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   ST_REQUIRE(fd >= 0, "st_comm_unique_id: socket: %s", std::strerror(errno));
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
