@@ -29,6 +29,9 @@ of 64*N, rows split in contiguous blocks, one RCCL all-gather per round.
 
 Extra objects on the JSON line:
   roofline         the round's kernels (HIP events on the launch stream)
+  round_distribution  (N = 1) per-round HIP-event times of a second pass of
+                   the same schedule (first / median / max, first and last
+                   5) and the GPU's clock levels around both passes
   solve            the reference-semantics solve to convergence (rounds, λ)
   matrix_free      the read-only form of the iteration,
                    priced against its own N^2*b bytes
@@ -362,6 +365,58 @@ def host_info() -> dict:
             "cgroup_cpu_quota": quota, "omp_num_threads": omp, "threads": threads}
 
 
+def gpu_clocks(torch, index: int = 0):
+    """The GPU's current shader / memory / fabric clock levels, read from the
+    amdgpu driver's sysfs files of this device's PCI function (the starred
+    line of pp_dpm_sclk / pp_dpm_mclk / pp_dpm_fclk); None where unreadable."""
+    try:
+        pr = torch.cuda.get_device_properties(index)
+        pci = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+    except Exception:   # noqa: BLE001 - no PCI identity: no reading
+        return None
+    out = {"pci": pci}
+    for key in ("sclk", "mclk", "fclk"):
+        try:
+            lines = open(f"/sys/bus/pci/devices/{pci}/pp_dpm_{key}").read().splitlines()
+            cur = [ln for ln in lines if ln.rstrip().endswith("*")]
+            out[key] = cur[0].split(":", 1)[-1].replace("*", "").strip() if cur else None
+        except OSError:
+            out[key] = None
+    return out
+
+
+def round_distribution(sh, kind, steps, warmup, torch):
+    """Per-round HIP-event times of a second pass of the bench's exact
+    schedule (fresh A_0, W warm-up rounds, K rounds), one event between
+    rounds: whether the first timed rounds run slower than the rest (a ramp
+    inside a short K) shows here.  A separate pass, so that the events
+    between rounds stay out of the timed region whose K rounds give
+    `value`."""
+    sh.load(kind)
+    cool_down(torch)
+    sh.start()
+    for _ in range(warmup):
+        sh.round(0.0, BIG)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    torch.cuda.synchronize()
+    clk0 = gpu_clocks(torch, torch.cuda.current_device())
+    ev[0].record()
+    for k in range(steps):
+        sh.round(0.0, BIG)
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    clk1 = gpu_clocks(torch, torch.cuda.current_device())
+    ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(steps)]
+    srt = sorted(ms)
+    return {"first": round(ms[0], 5), "median": round(srt[len(srt) // 2], 5),
+            "max": round(srt[-1], 5), "min": round(srt[0], 5),
+            "mean": round(sum(ms) / len(ms), 5), "first5": [round(x, 5) for x in ms[:5]],
+            "last5": [round(x, 5) for x in ms[-5:]],
+            "clocks_before": clk0, "clocks_after": clk1,
+            "timing": ("a second pass of the same schedule (fresh A_0, W warm-up rounds, "
+                       "K rounds) with a HIP event between rounds; not the timed region")}
+
+
 # ---------------------------------------------------------------------------
 # timing
 # ---------------------------------------------------------------------------
@@ -374,7 +429,10 @@ def _max_over_ranks(torch, dist, world, *vals):
     return tuple(float(x) for x in t)
 
 
-def timed_rounds(sh, steps, warmup, torch, dist, world):
+CLOCKS = {}   # GPU clock levels around the headline's timed region (rank 0, N = 1)
+
+
+def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     """Warmup + K timed rounds; returns (elapsed_s_max, kernel_ms_avg).
 
     The kernel's average launch duration comes from HIP events recorded on
@@ -393,6 +451,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if clocks_key:
+        CLOCKS[clocks_key + "_before"] = gpu_clocks(torch, torch.cuda.current_device())
     t0 = time.perf_counter()
     if world == 1:
         ev[0][0].record()
@@ -405,6 +465,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world):
         dist.barrier()
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
+    if clocks_key:
+        CLOCKS[clocks_key + "_after"] = gpu_clocks(torch, torch.cuda.current_device())
     if world == 1:
         return el, ev[0][0].elapsed_time(ev[0][1]) / steps
     n_ev = min(steps, 50)
@@ -1095,7 +1157,8 @@ def main():
 
     # ---- timed rounds ----------------------------------------------------
     sh.load(args.kind, mat=None)
-    el, fused_ms = timed_rounds(sh, args.steps, args.warmup, torch, dist, world)
+    el, fused_ms = timed_rounds(sh, args.steps, args.warmup, torch, dist, world,
+                                clocks_key="headline")
     bytes_round_total = 2.0 * n * n * b
     bytes_round_local = 2.0 * p.nrows * n * b
     value = bytes_round_total * args.steps / el / 1e9
@@ -1150,6 +1213,16 @@ def main():
         ov.close()
         del ov, tgt
         progress(f"headline pass ({schedule}): {el / args.steps * 1e3:.5f} ms per round")
+
+    # ---- the per-round distribution of the same schedule (a second pass) ----
+    dist_rounds = None
+    if world == 1:
+        dist_rounds = round_distribution(sh, args.kind, args.steps, args.warmup, torch)
+        dist_rounds["headline_clocks"] = dict(CLOCKS)
+        dist_rounds["headline_events_ms_per_round"] = round(fused_ms, 5)
+        dist_rounds["headline_host_ms_per_round"] = round(el / args.steps * 1e3, 5)
+        progress(f"per-round distribution: first {dist_rounds['first']} median "
+                 f"{dist_rounds['median']} max {dist_rounds['max']} ms")
 
     use_overlap = schedule == "overlapped"
     flat_pays = dev.flat_round_pays(p.nrows, n, dt)
@@ -1243,6 +1316,8 @@ def main():
         out["rccl_ranks"] = exchange["rccl_ranks"]
     if overlap_leg is not None:
         out["exchange_other_schedule"] = overlap_leg
+    if dist_rounds is not None:
+        out["round_distribution"] = dist_rounds
     if weak_blocks is not None:
         out["weak_rank_blocks"] = weak_blocks
     sh.close()

@@ -21,6 +21,7 @@ ST_FLAG_TIME_KERNELS = 1
 ST_FLAG_MATRIX_FREE = 2
 ST_FLAG_ROUND_LOOP = 4
 ST_FLAG_WRITE_EVERY_ROUND = 8
+ST_FLAG_TRACE_SUMS = 16
 ST_MAX_ITR = 1000
 
 DTYPE_F32 = 0
@@ -62,7 +63,9 @@ class st_launch_policy(ctypes.Structure):
 
 
 ST_FORM_ROUND, ST_FORM_DEFER_READ, ST_FORM_DEFER_STORE, ST_FORM_MFREE = 0, 1, 2, 3
-KERNEL_NAMES = {0: "k_round", 1: "k_flat", 2: "k_flat<NP>", 3: "k_mfree"}
+ST_FORM_ROWSUM = 4
+KERNEL_NAMES = {0: "k_round", 1: "k_flat", 2: "k_flat<NP>", 3: "k_mfree", 4: "k_fused",
+                5: "k_flat_sum"}
 
 
 def launch_policy(dtype: str, nrows: int, ncols: int, form: int, npend: int = 0) -> dict:
@@ -148,6 +151,8 @@ def _declare(L: ctypes.CDLL) -> None:
     L.max_eigen_value_ex.restype = i64
     L.st_last_round_times.argtypes = [P, P, u32]
     L.st_last_round_times.restype = i32
+    L.st_last_round_sums.argtypes = [P, P, u32]
+    L.st_last_round_sums.restype = i32
     L.st_set_stream.argtypes = [P, P]
     L.st_set_stream.restype = i32
     L.st_use_own_stream.argtypes = [P]
@@ -164,6 +169,7 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"st_generate_identity_{sfx}").argtypes = [P, u32, u32, u32, P]
         getattr(L, f"st_fill_{sfx}").argtypes = [P, u64, T, P]
         getattr(L, f"st_rowsum_{sfx}").argtypes = [P, P, u32, u32, P]
+        getattr(L, f"st_rowsum_flat_{sfx}").argtypes = [P, P, P, u32, u32, P]
         getattr(L, f"st_scale_rowsum_{sfx}").argtypes = [P, P, P, u32, u32, u32, u32, P, P]
         getattr(L, f"st_epilogue_{sfx}").argtypes = [P, P, u32, T, u32, u32, P, P]
         getattr(L, f"st_round_{sfx}").argtypes = [P, P, P, P, u32, u32, u32, T, u32, u32,
@@ -184,7 +190,7 @@ def _declare(L: ctypes.CDLL) -> None:
             P, P, P, P, P, P, P, u32, u32, u32, T, u32, u32, u32, P, P, u32, i32, i32, P, P]
         getattr(L, f"st_recip_{sfx}").argtypes = [P, P, u32, P]
         for name in ("generate_hilbert", "generate_random", "generate_identity",
-                     "fill", "rowsum", "scale_rowsum", "epilogue", "round", "mfree_round",
+                     "fill", "rowsum", "rowsum_flat", "scale_rowsum", "epilogue", "round", "mfree_round",
                      "round_split", "round_split_flat", "round_flat", "round_flat_deferred",
                      "recip"):
             getattr(L, f"st_{name}_{sfx}").restype = i32
@@ -239,6 +245,16 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_launch_policy_query.restype = i32
     L.st_state_reset.argtypes = [P, P]
     L.st_state_reset.restype = i32
+
+
+def round_sums(L: ctypes.CDLL, q, n: int, dtype):
+    """st_last_round_sums of queue ``q`` as a (rounds, n) array of ``dtype``."""
+    import numpy as np
+    r = check(L.st_last_round_sums(q, None, 0), "st_last_round_sums", L)
+    out = np.zeros((r, n), dtype=dtype)
+    if r and n:
+        check(L.st_last_round_sums(q, out.ctypes.data, r), "st_last_round_sums", L)
+    return out
 
 
 def rccl_info(L: Optional[ctypes.CDLL] = None) -> dict:

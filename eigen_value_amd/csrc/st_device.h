@@ -1393,6 +1393,86 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   }
 }
 
+// K0 in the flat form, s_0 = A_0 1 (similarity_transform.cpp:40, the first
+// sum_across_rows before the loop's first stop test) for blocks where the
+// flat round pays: one short workgroup per (R rows, column piece) writes the
+// piece's partial sums, k_parts then sums each row's pieces in a fixed order
+// - deterministic and independent of the row partition, as the rounds' row
+// sums are.  Read-only and ungated: the loads and walk order of the deferred
+// form's read-only round with nothing pending (pt: tiles of pt row groups per
+// piece, 0 = row-major), without its scaling.  Replaces the grid-stride
+// k_fused launch, which streamed the same bytes at 0.77 / 0.83 of 8 TB/s
+// (8192^2 / 32768^2 fp64) where the flat read-only round ran 0.88 / 0.90.
+template <typename T, int W, bool NT, int R, int U, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void
+k_flat_sum(const T* __restrict__ a, T* __restrict__ part, uint32_t nrows,
+           uint32_t ncols, uint32_t ppr, uint32_t pt, uint32_t gx2)
+{
+  using V = typename vec<T, W>::type;
+  constexpr int NW = BLK / 64;
+  __shared__ T red[NW][R];
+  const uint32_t ng = (nrows + R - 1) / R;
+  uint32_t b = blockIdx.x;
+  if (gx2 != 0) { // a 2-D grid (k_flat's gx2): fold blockIdx.y back in
+    b += blockIdx.y * gx2;
+    if (b >= ng * ppr)
+      return;
+  }
+  uint32_t rg, p;
+  if (pt != 0) { // pt row groups of one piece back to back (k_flat's order)
+    const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
+    const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;
+    p = t / g;
+    rg = tile * pt + (t - p * g);
+  } else {
+    rg = b / ppr;
+    p = b - rg * ppr;
+  }
+  const uint32_t c0 = (p * (uint32_t)(BLK * U) + threadIdx.x) * W;
+  const uint32_t r0 = rg * R;
+  const size_t lda = (size_t)ncols;
+  V x[U][R];
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (c0 + u * BLK * W < ncols && r0 + j < nrows)
+        x[u][j] = ld<V, NT>(reinterpret_cast<const V*>(a + (size_t)(r0 + j) * lda + c0 +
+                                                       u * BLK * W));
+  }
+  T acc[R];
+#pragma unroll
+  for (int j = 0; j < R; j++) {
+    acc[j] = (T)0;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (c0 + u * BLK * W < ncols && r0 + j < nrows)
+        acc[j] = u == 0 ? hsum<T, W>(x[u][j]) : acc[j] + hsum<T, W>(x[u][j]);
+  }
+  // the wave sums land in lanes 62 / 63 (k_flat's trees), then the waves'
+  // sums in wave order
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j + 1 < R; j += 2) {
+    const T t = wave_sum_pair(acc[j], acc[j + 1]);
+    if (lane >= 62)
+      red[wave][j + (lane - 62)] = t;
+  }
+  if constexpr (R % 2 == 1) {
+    const T t = wave_sum_l63(acc[R - 1]);
+    if (lane == 63)
+      red[wave][R - 1] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < R && r0 + threadIdx.x < nrows) {
+    T t = red[0][threadIdx.x];
+#pragma unroll
+    for (int w = 1; w < NW; w++)
+      t += red[w][threadIdx.x];
+    part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
+  }
+}
+
 // The solve loops' per-batch look at the state: one wave copies the 64 B
 // st_state into the caller's pinned, host-coherent slot with vector stores
 // (16 lanes, one word each), in stream order behind the batch's rounds.  It
@@ -1495,7 +1575,7 @@ k_parts_seg(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   // whole waves stay together (DPP reads neighbours): rows past the block
   // compute on zeros and store nothing
   const bool live = r < nrows;
-  const uint32_t e = state->end;
+  const uint32_t e = state != nullptr ? state->end : 0u; // no state: K0, ungated
   T vr = (T)0, sr = (T)1, m = (T)1;
   if (v != nullptr && seg == LPR - 1 && live) {
     vr = v[row0 + r];
@@ -1544,7 +1624,7 @@ k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   const uint32_t lane = threadIdx.x & 63;
   if (r >= nrows)
     return; // whole waves leave together
-  const uint32_t e = state->end;
+  const uint32_t e = state != nullptr ? state->end : 0u; // no state: K0, ungated
   T vr = (T)0, sr = (T)1, m = (T)1;
   if (v != nullptr && lane == 0) {
     vr = v[row0 + r];

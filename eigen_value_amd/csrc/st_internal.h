@@ -61,6 +61,11 @@ struct DeviceGuard
 template <typename T>
 int launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
                   hipStream_t stream);
+// K0 in the flat form (k_flat_sum + k_parts) for blocks where the flat round
+// pays; `part` holds round_flat_scratch(nrows, ncols) elements
+template <typename T>
+int launch_rowsum_flat(const T* a, T* s, T* part, uint32_t nrows,
+                       uint32_t ncols, hipStream_t stream);
 template <typename T>
 int launch_scale_rowsum(T* a, const T* s_cur, T* s_next, uint32_t nrows,
                         uint32_t ncols, uint32_t row0, uint32_t semantics,

@@ -1374,6 +1374,59 @@ launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
   return check_launch("rowsum");
 }
 
+// K0 in the flat form (k_flat_sum + k_parts) for blocks where the flat round
+// pays: the pieces (kFlatU), rows per workgroup and walk order (defer_rows /
+// defer_tile), workgroups-per-CU cap and load policy (g_defer_flip bit 0) of
+// the deferred form's read-only round with nothing pending, which streams
+// the same bytes - a matrix just written, like A_0 after its generator or
+// copy - without the scaling.  k_parts runs ungated (no state).
+template <typename T, int W, bool NT>
+void
+launch_rowsum_flat_cfg(const T* a, T* s, T* part, uint32_t nrows, uint32_t ncols,
+                       hipStream_t stream)
+{
+  constexpr int U = kFlatU<T, W, NT>;
+  constexpr int R = defer_rows<T, NT>(0, false);
+  const uint32_t ppr = flat_pieces(ncols, W * U);
+  const uint32_t pt = defer_tile<T, NT>(0, false);
+  const uint32_t lds = defer_lds<T, NT>(0);
+  const FlatGrid fg = flat_grid((nrows + R - 1) / R * ppr);
+  const bool flip = W > 1 && (defer_flip<T>(nrows, ncols) & 1u) != 0;
+  if (NT != flip)
+    hipLaunchKernelGGL((dev::k_flat_sum<T, W, true, R, U>), fg.grid, dim3(kBlock), lds,
+                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2);
+  else
+    hipLaunchKernelGGL((dev::k_flat_sum<T, W, false, R, U>), fg.grid, dim3(kBlock), lds,
+                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2);
+  launch_parts<T>(part, s, nrows, ppr, 0u, nullptr, nullptr, nullptr, 0u, nullptr, stream);
+}
+
+template <typename T>
+int
+launch_rowsum_flat(const T* a, T* s, T* part, uint32_t nrows, uint32_t ncols,
+                   hipStream_t stream)
+{
+  ST_REQUIRE(a && s && part, "rowsum_flat: null pointer");
+  if (nrows == 0)
+    return 0;
+  ST_REQUIRE(ncols > 0, "rowsum_flat: ncols must be > 0");
+  constexpr int W = 16 / sizeof(T);
+  const bool vec_ok = (ncols % W) == 0 && aligned16(a);
+  const bool nt = flat_round_nt(nrows, ncols, sizeof(T));
+  if (vec_ok)
+    nt ? launch_rowsum_flat_cfg<T, W, true>(a, s, part, nrows, ncols, stream)
+       : launch_rowsum_flat_cfg<T, W, false>(a, s, part, nrows, ncols, stream);
+  else
+    nt ? launch_rowsum_flat_cfg<T, 1, true>(a, s, part, nrows, ncols, stream)
+       : launch_rowsum_flat_cfg<T, 1, false>(a, s, part, nrows, ncols, stream);
+  return check_launch("rowsum_flat");
+}
+
+template int launch_rowsum_flat<float>(const float*, float*, float*, uint32_t, uint32_t,
+                                       hipStream_t);
+template int launch_rowsum_flat<double>(const double*, double*, double*, uint32_t,
+                                        uint32_t, hipStream_t);
+
 template <typename T>
 int
 launch_scale_rowsum(T* a, const T* s_cur, T* s_next, uint32_t nrows,
@@ -1585,6 +1638,16 @@ policy_flat(uint32_t nrows, uint32_t ncols, int form, uint32_t np,
     o->store_nt = NT != ((pol & 2u) != 0);
     return 0;
   }
+  if (form == ST_FORM_ROWSUM) { // K0: launch_rowsum_flat_cfg
+    o->kernel = ST_KERNEL_FLAT_SUM;
+    o->rows = defer_rows<T, NT>(0, false);
+    o->tile = defer_tile<T, NT>(0, false);
+    o->cap = g_defer_caps[sizeof(T) == 8][NT][0].load(std::memory_order_relaxed);
+    o->load_nt = NT != ((defer_flip<T>(nrows, ncols) & 1u) != 0);
+    o->store_nt = -1;
+    o->alt = 0;
+    return 0;
+  }
   const bool store = form == ST_FORM_DEFER_STORE;
   ST_REQUIRE(np < kDeferRoundsMax && (store || np + 1 < kDeferRoundsMax),
              "st_launch_policy: %u pending rounds %s", np,
@@ -1614,6 +1677,16 @@ policy(uint32_t nrows, uint32_t ncols, int form, uint32_t np, st_launch_policy* 
     o->load_nt = sh.nt;
     o->store_nt = -1;
     o->alt = 1;
+    return 0;
+  }
+  if (form == ST_FORM_ROWSUM && !round_flat_pays(nrows, ncols, sizeof(T))) {
+    // K0 below the flat round: k_fused (launch_rows)
+    const bool nt = fused_nt(nrows, ncols, sizeof(T));
+    o->kernel = ST_KERNEL_FUSED;
+    o->rows = nrows < 2 * kGridCap ? 1 : nt ? 4 : kRows;
+    o->grid = kGridCap;
+    o->load_nt = nt;
+    o->store_nt = -1;
     return 0;
   }
   if (!round_flat_pays(nrows, ncols, sizeof(T))) {
@@ -1687,6 +1760,14 @@ st_state_reset(st_state* d_state, void* stream)
   {                                                                            \
     st::clear_error();                                                         \
     return st::launch_rowsum<T>(d_mat, d_s, nrows, ncols, ST_STREAM(stream)); \
+  }                                                                            \
+  int st_rowsum_flat_##SFX(const T* d_mat, T* d_s, T* d_part,                  \
+                           unsigned int nrows, unsigned int ncols,             \
+                           void* stream)                                       \
+  {                                                                            \
+    st::clear_error();                                                         \
+    return st::launch_rowsum_flat<T>(d_mat, d_s, d_part, nrows, ncols,         \
+                                     ST_STREAM(stream));                       \
   }                                                                            \
   int st_scale_rowsum_##SFX(T* d_mat, const T* d_s_cur, T* d_s_next,           \
                             unsigned int nrows, unsigned int ncols,            \
@@ -1860,7 +1941,7 @@ st_launch_policy_query(int dtype, unsigned int nrows, unsigned int ncols, int fo
   ST_REQUIRE(dtype == 0 || dtype == 1, "st_launch_policy: dtype 0 (fp32) or 1 (fp64)");
   ST_REQUIRE(nrows > 0 && ncols > 0 && ncols % (dtype == 1 ? 2u : 4u) == 0,
              "st_launch_policy: a block of whole 16-byte chunks per row");
-  ST_REQUIRE(form >= ST_FORM_ROUND && form <= ST_FORM_MFREE, "st_launch_policy: form 0..3");
+  ST_REQUIRE(form >= ST_FORM_ROUND && form <= ST_FORM_ROWSUM, "st_launch_policy: form 0..4");
   return dtype == 1 ? st::policy<double>(nrows, ncols, form, npend, out)
                     : st::policy<float>(nrows, ncols, form, npend, out);
 }

@@ -435,9 +435,11 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
     for (int i = 0; i < (mfree ? 2 : 1); i++)
       ST_CHECK(hipMalloc(&d.v[i], sizeof(T) * (size_t)P * chunk));
     ST_CHECK(hipMalloc(&d.state, sizeof(st_state)));
-    if (!mfree && round_flat_pays(d.nrows, n, sizeof(T)))
+    // the flat-form scratch: the flat rounds' and K0's (the matrix-free
+    // loop's K0 too)
+    if (round_flat_pays(d.nrows, n, sizeof(T)))
       ST_CHECK(hipMalloc(&d.part, sizeof(T) * round_flat_scratch(d.nrows, n)));
-    d.defer = d.part != nullptr && !every;
+    d.defer = d.part != nullptr && !every && !mfree;
     if (d.defer)
       for (uint32_t i = 0; i < nring; i++)
         ST_CHECK(hipMalloc(&d.inv[i], sizeof(T) * (size_t)P * chunk));
@@ -473,7 +475,7 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   ST_CHECK(hipEventCreateWithFlags(&M.ev[0], hipEventDisableTiming));
   ST_CHECK(hipEventCreateWithFlags(&M.ev[1], hipEventDisableTiming));
   if (batch == 0) // as st_solve.hip: flat rounds are checked every 2 rounds
-    batch = M.sh[0].part ? 2u : 8u;
+    batch = (M.sh[0].part && !mfree) ? 2u : 8u;
   {
     // ncclCommInitAll, but under the deadline: one id, a group of
     // per-device non-blocking ncclCommInitRankConfig calls on a helper
@@ -519,7 +521,9 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
   for (uint32_t p = 0; p < P; p++) { // s_0 = rowsum(A_0), then gather
     Shard<T>& d = M.sh[p];
     ST_CHECK(hipSetDevice(d.dev));
-    if (launch_rowsum<T>(d.a, d.s[0] + p * chunk, d.nrows, n, d.stream))
+    if (d.part ? launch_rowsum_flat<T>(d.a, d.s[0] + p * chunk, d.part, d.nrows, n,
+                                       d.stream)
+               : launch_rowsum<T>(d.a, d.s[0] + p * chunk, d.nrows, n, d.stream))
       return -1;
   }
   if (gather(M, 0, chunk))
@@ -574,7 +578,7 @@ solve_multi(const T* mat, uint32_t n, int ngpus, const int* devices,
             d.inv[nxt] + d.row0, d.part, d.v[0], d.nrows, n, d.row0, eps, k,
             max_itr, sem, d.state, ps, pi, np, np + 1 == kDefer, false,
             d.stream);
-        } else if (d.part)
+        } else if (d.part) // (never matrix-free: that branch comes first)
           rc = launch_round_flat<T>(d.a, d.s[cur], d.s[nxt] + p * chunk,
                                     d.part, d.v[0], d.nrows, n, d.row0, eps, k,
                                     max_itr, sem, d.state, d.stream);

@@ -7,6 +7,7 @@
 //
 // Round loop (one device stream, no per-round host sync):
 //   K0  s_0 = rowsum(A_0)                                  N^2 b read, once
+//       (k_flat_sum + k_parts where the flat round pays, else k_fused)
 //   per round k, ONE launch (k_round, st_device.h; matrices of >= 144 MiB
 //   take the flat round, k_flat + k_parts, instead, storing the matrix
 //   every defer_rounds() rounds; N <= 128 fp64 / 256 fp32 run the whole
@@ -75,6 +76,13 @@ struct Context
   st_state* d_state = nullptr;
   st_state* h_state = nullptr; // pinned, 2 slots
   std::vector<float> round_ms; // per-round kernel time of the last timed solve
+  // ST_FLAG_TRACE_SUMS: the row sums s_k every round of the last traced
+  // solve evaluated (device staging, then the host copy st_last_round_sums
+  // returns)
+  void* d_trace = nullptr;
+  size_t trace_cap = 0;
+  std::vector<unsigned char> trace;
+  uint32_t trace_rounds = 0;
   hipEvent_t ev_flag[2] = { nullptr, nullptr };
 };
 
@@ -138,6 +146,26 @@ ensure_matrix(Context* c, size_t bytes)
   }
   ST_CHECK(hipMalloc(&c->d_mat, bytes));
   c->mat_bytes = bytes;
+  return 0;
+}
+
+// a traced solve records every evaluated round's n row sums: at most
+// kTraceMaxBytes of them (tests and diagnostics, not a production mode)
+constexpr size_t kTraceMaxBytes = (size_t)1 << 30;
+
+int
+ensure_trace(Context* c, size_t bytes)
+{
+  if (c->d_trace && c->trace_cap >= bytes)
+    return 0;
+  if (c->d_trace) {
+    ST_CHECK(hipStreamSynchronize(c->stream));
+    ST_CHECK(hipFree(c->d_trace));
+    c->d_trace = nullptr;
+    c->trace_cap = 0;
+  }
+  ST_CHECK(hipMalloc(&c->d_trace, bytes));
+  c->trace_cap = bytes;
   return 0;
 }
 
@@ -205,6 +233,17 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   T* d_v2 = reinterpret_cast<T*>((char*)c->d_vec + 3 * c->vec_bytes);
   T* vb[2] = { d_v, d_v2 };
   const bool timed = (o.flags & ST_FLAG_TIME_KERNELS) != 0;
+  const bool traced = (o.flags & ST_FLAG_TRACE_SUMS) != 0;
+  const size_t row_bytes = sizeof(T) * (size_t)n;
+  c->trace.clear();
+  c->trace_rounds = 0;
+  if (traced) {
+    ST_REQUIRE(row_bytes * o.max_itr <= kTraceMaxBytes,
+               "ST_FLAG_TRACE_SUMS: %u rounds x %u row sums exceed the %zu MiB "
+               "trace; lower max_itr", o.max_itr, n, kTraceMaxBytes >> 20);
+    if (ensure_trace(c, row_bytes * o.max_itr))
+      return -1;
+  }
   const bool mfree = (o.flags & ST_FLAG_MATRIX_FREE) != 0;
   // large matrices: the flat round (k_flat + k_parts)
   const bool flat = !mfree && round_flat_pays(n, n, sizeof(T));
@@ -220,7 +259,10 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     ring_inv[i] = reinterpret_cast<T*>((char*)c->d_vec +
                                        (4 + kDeferRoundsMax + 1 + i) * c->vec_bytes);
   }
-  if (flat && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
+  // K0 takes the flat form wherever the flat round pays (the matrix-free
+  // loop's too)
+  const bool flat_k0 = round_flat_pays(n, n, sizeof(T));
+  if (flat_k0 && ensure_part(c, sizeof(T) * round_flat_scratch(n, n)))
     return -1;
   T* d_part = reinterpret_cast<T*>(c->d_part);
   // rounds per host flag check: the launches queued behind the stopping
@@ -249,9 +291,9 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
   int rc = 0;
 
   // a matrix that fits one workgroup's registers runs the whole solve in a
-  // single launch, bit-identical to the round loop below; per-round timing
-  // and ST_FLAG_ROUND_LOOP keep the loop
-  const bool single = !mfree && !timed && (o.flags & ST_FLAG_ROUND_LOOP) == 0 &&
+  // single launch, bit-identical to the round loop below; per-round timing,
+  // tracing and ST_FLAG_ROUND_LOOP keep the loop
+  const bool single = !mfree && !timed && !traced && (o.flags & ST_FLAG_ROUND_LOOP) == 0 &&
                       solve_small_fits<T>(d_mat, n);
   const auto t0 = std::chrono::steady_clock::now();
   ST_CHECK(hipMemsetAsync(c->d_state, 0, sizeof(st_state), s));
@@ -263,7 +305,9 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
       return -1;
     (void)hipEventRecord(ev[0], s);
   }
-  if (!single && launch_rowsum<T>(d_mat, defer ? ring_s[0] : s_buf[0], n, n, s)) // K0
+  T* const s0 = defer ? ring_s[0] : s_buf[0];
+  if (!single && (flat_k0 ? launch_rowsum_flat<T>(d_mat, s0, d_part, n, n, s)
+                          : launch_rowsum<T>(d_mat, s0, n, n, s))) // K0
     return -1;
   if (defer && launch_recip<T>(ring_s[0], ring_inv[0], n, s))
     return -1;
@@ -285,6 +329,10 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     for (uint32_t j = 0; j < b; j++) {
       const uint32_t k = enqueued + j;
       hipEvent_t ea = nullptr, eb = nullptr;
+      if (traced) // s_k, the row sums round k evaluates (no-op copies past the stop)
+        rc |= hipMemcpyAsync((char*)c->d_trace + (size_t)k * row_bytes,
+                             defer ? ring_s[k % kR] : s_buf[cur], row_bytes,
+                             hipMemcpyDeviceToDevice, s) != hipSuccess;
       if (timed) {
         rc |= mk(&ea) | mk(&eb);
         ev.push_back(ea);
@@ -368,6 +416,12 @@ solve_device(Context* c, T* d_mat, uint32_t n, T* d_v_out, T* v_host,
     ST_CHECK(hipMemcpy(v_host, d_v, sizeof(T) * (size_t)n,
                        hipMemcpyDeviceToHost));
   const double d2h_ms = ms_since(t1);
+  if (traced) { // rounds 0 .. end-1 were evaluated
+    c->trace.resize(row_bytes * fin.end);
+    ST_CHECK(hipMemcpy(c->trace.data(), c->d_trace, c->trace.size(),
+                       hipMemcpyDeviceToHost));
+    c->trace_rounds = fin.end;
+  }
 
   // per-round kernel times (rounds 0 .. end-1 did work; the stop round's
   // launch also streams the matrix), kept for st_last_round_times
@@ -525,6 +579,8 @@ destroy_queue(void* wq)
     (void)hipFree(c->d_vec);
   if (c->d_part)
     (void)hipFree(c->d_part);
+  if (c->d_trace)
+    (void)hipFree(c->d_trace);
   if (c->d_state)
     (void)hipFree(c->d_state);
   if (c->h_state)
@@ -548,6 +604,21 @@ st_last_round_times(void* wq, float* ms, unsigned int cap)
   for (size_t i = 0; i < n && i < cap; i++)
     ms[i] = c->round_ms[i];
   return (int)n;
+}
+
+int
+st_last_round_sums(void* wq, void* sums, unsigned int cap_rounds)
+{
+  st::clear_error();
+  Context* c = st::as_ctx(wq);
+  ST_REQUIRE(c, "st_last_round_sums: null queue");
+  ST_REQUIRE(sums || cap_rounds == 0, "st_last_round_sums: null buffer");
+  const uint32_t r = c->trace_rounds;
+  if (r && cap_rounds) {
+    const size_t row = c->trace.size() / r;
+    std::memcpy(sums, c->trace.data(), row * (cap_rounds < r ? cap_rounds : r));
+  }
+  return (int)r;
 }
 
 int

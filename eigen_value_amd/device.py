@@ -113,6 +113,16 @@ def rowsum(mat, out=None):
     return out
 
 
+def rowsum_flat(mat, out, part) -> None:
+    """out[r] = sum_c mat[r][c] in the flat form (st_rowsum_flat): the
+    solve loops' initial pass for blocks where ``flat_round_pays``; ``part``
+    is ``flat_scratch(nrows, ncols)``."""
+    _check_cuda(mat, out, part)
+    _lib.check(getattr(_lib.load(), f"st_rowsum_flat_{_sfx(mat)}")(
+        _ptr(mat), _ptr(out), _ptr(part), mat.shape[0], mat.shape[1],
+        _stream(mat.device)), "rowsum_flat")
+
+
 def scale_rowsum(mat, s_cur, s_next=None, row0: int = 0,
                  semantics: int = _lib.ST_SEM_SYCL, state=None) -> None:
     """Fused round body, in place on ``mat`` (local rows row0..): see
@@ -346,7 +356,8 @@ class DeviceSolver:
     def solve(self, mat, *, inplace: bool = False, eps: Optional[float] = None,
               max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL, batch: int = 0,
               time_kernels: bool = False, matrix_free: bool = False,
-              round_loop: bool = False, write_every_round: bool = False):
+              round_loop: bool = False, write_every_round: bool = False,
+              trace_sums: bool = False):
         """Returns (λ: float, v: tensor, iterations: int, stats: dict).
 
         Matrices of n <= 128 (fp64) / 256 (fp32) run the whole solve in one
@@ -365,7 +376,9 @@ class DeviceSolver:
         reference loop, which breaks before compute_next_matrix (cpp:45-52).
         ``matrix_free`` runs the read-only form: the
         input is never written, so no copy is made.  ``mat`` may be a torch
-        tensor or any DLPack producer (``__dlpack__``) on this device."""
+        tensor or any DLPack producer (``__dlpack__``) on this device.
+        ``trace_sums`` records every evaluated round's row sums
+        (``ST_FLAG_TRACE_SUMS``; identical results): ``last_round_sums()``."""
         torch = _torch()
         if not isinstance(mat, torch.Tensor) and hasattr(mat, "__dlpack__"):
             mat = torch.from_dlpack(mat)   # any DLPack producer, zero copy
@@ -385,16 +398,26 @@ class DeviceSolver:
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
                  | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
                  | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0)
-                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0))
+                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0)
+                 | (_lib.ST_FLAG_TRACE_SUMS if trace_sums else 0))
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()
+        self._trace = (n, mat.dtype)
         _lib.check(self.L.st_set_stream(self.q, _stream(mat.device)), "st_set_stream")
         rc = getattr(self.L, f"st_solve_device_{_sfx(mat)}")(
             self.q, _ptr(work), n, _ptr(v), None, ctypes.byref(ev), ctypes.byref(it),
             ctypes.byref(opt), ctypes.byref(stats))
         _lib.check(rc, "st_solve_device")
         return float(ev.value), v, int(it.value), stats.as_dict()
+
+    def last_round_sums(self):
+        """Row sums s_0 .. s_{rounds-1} of the last ``solve(trace_sums=True)``
+        as a (rounds, n) numpy array (empty if that solve was not traced)."""
+        import numpy as np
+        n, dt = getattr(self, "_trace", (0, None))
+        npdt = np.float64 if dt is not None and dt == _torch().float64 else np.float32
+        return _lib.round_sums(self.L, self.q, n, npdt)
 
     def close(self) -> None:
         if self.q is not None and self.q.value:

@@ -87,8 +87,21 @@ class HipShardOps:
     def fill(self, x, value):
         self.dev.fill(x, value)
 
+    def _scratch(self, nrows, ncols, dtype):
+        key = (nrows, ncols, dtype)
+        if self._part is None or self._part[0] != key:
+            self._part = (key, self.dev.flat_scratch(nrows, ncols, dtype, self.device))
+        return self._part[1]
+
     def rowsum(self, mat, out):
-        if mat.shape[0]:
+        # K0: the flat form where the flat round pays (st_rowsum_flat), as
+        # the library's own solve loops run it
+        nrows, ncols = mat.shape
+        if not nrows:
+            return
+        if self.dev.flat_round_pays(nrows, ncols, mat.dtype):
+            self.dev.rowsum_flat(mat, out, self._scratch(nrows, ncols, mat.dtype))
+        else:
             self.dev.rowsum(mat, out=out)
 
     def scale_rowsum(self, mat, s_cur, s_next, row0, semantics, state):
@@ -104,10 +117,8 @@ class HipShardOps:
         # one-launch k_round
         nrows, ncols = mat.shape
         if self.dev.flat_round_pays(nrows, ncols, mat.dtype):
-            key = (nrows, ncols, mat.dtype)
-            if self._part is None or self._part[0] != key:
-                self._part = (key, self.dev.flat_scratch(nrows, ncols, mat.dtype, self.device))
-            self.dev.flat_round(mat, s_cur, s_next, self._part[1], v, state, row0=row0,
+            self.dev.flat_round(mat, s_cur, s_next, self._scratch(nrows, ncols, mat.dtype),
+                                v, state, row0=row0,
                                 eps=eps, k=k, max_itr=max_itr, semantics=semantics)
         else:
             self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
@@ -144,10 +155,8 @@ class HipShardOps:
     def round_deferred(self, mat, s_cur, inv_cur, s_next, inv_next, v, pend_s, pend_inv,
                        row0, eps, k, max_itr, semantics, state, store, flush=False):
         nrows, ncols = mat.shape
-        key = (nrows, ncols, mat.dtype)
-        if self._part is None or self._part[0] != key:
-            self._part = (key, self.dev.flat_scratch(nrows, ncols, mat.dtype, self.device))
-        self.dev.flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next, self._part[1], v,
+        self.dev.flat_round_deferred(mat, s_cur, inv_cur, s_next, inv_next,
+                                     self._scratch(nrows, ncols, mat.dtype), v,
                                      state, pend_s, pend_inv, store=store, flush=flush,
                                      row0=row0, eps=eps, k=k, max_itr=max_itr,
                                      semantics=semantics)

@@ -76,13 +76,15 @@ class EigenValue:
                                 max_itr: int = 0, semantics: int = _lib.ST_SEM_SYCL,
                                 batch: int = 0, time_kernels: bool = False,
                                 matrix_free: bool = False, round_loop: bool = False,
-                                write_every_round: bool = False):
+                                write_every_round: bool = False, trace_sums: bool = False):
         """Extended call: options + statistics (``max_eigen_value_ex``).
         ``round_loop`` keeps one launch per round where the whole solve would
         fit one workgroup (``ST_FLAG_ROUND_LOOP``; identical results);
         ``write_every_round`` stores the matrix every round where the flat
         round would store it every 6th (``ST_FLAG_WRITE_EVERY_ROUND``;
-        identical results).
+        identical results); ``trace_sums`` records every evaluated round's
+        row sums (``ST_FLAG_TRACE_SUMS``; identical results), read back with
+        ``last_round_sums()``.
 
         Returns ``(λ, v, ts_ms, iterations, stats_dict)``."""
         m, n = mat.shape
@@ -93,7 +95,9 @@ class EigenValue:
         flags = ((_lib.ST_FLAG_TIME_KERNELS if time_kernels else 0)
                  | (_lib.ST_FLAG_MATRIX_FREE if matrix_free else 0)
                  | (_lib.ST_FLAG_ROUND_LOOP if round_loop else 0)
-                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0))
+                 | (_lib.ST_FLAG_WRITE_EVERY_ROUND if write_every_round else 0)
+                 | (_lib.ST_FLAG_TRACE_SUMS if trace_sums else 0))
+        self._trace = (n, mat.dtype)
         opt = _lib.st_options(-1.0 if eps is None else float(eps), max_itr, semantics,
                               batch, flags)
         stats = _lib.st_stats()
@@ -118,6 +122,13 @@ class EigenValue:
             _lib.check(L.st_last_round_times(self.sycl_q, out.ctypes.data, n),
                        "st_last_round_times", L)
         return out
+
+    def last_round_sums(self) -> np.ndarray:
+        """Row sums s_0 .. s_{rounds-1} of the last ``similarity_transform_ex``
+        call made with ``trace_sums=True``, shape (rounds, n) (empty
+        otherwise)."""
+        n, dt = getattr(self, "_trace", (0, np.float32))
+        return _lib.round_sums(self.so_lib, self.sycl_q, n, dt)
 
     # ------------------------------------------------------------------
     def close(self) -> None:

@@ -99,6 +99,9 @@ typedef struct st_options
 #define ST_FLAG_ROUND_LOOP 4u   /* one launch per round even where the whole */
                                 /* solve fits one workgroup (n <= 128 fp64, */
                                 /* 256 fp32): results are identical        */
+#define ST_FLAG_TRACE_SUMS 16u  /* record every evaluated round's row sums  */
+                                /* s_k (st_last_round_sums; max_itr * dim   */
+                                /* elements <= 1 GiB): identical results    */
 
 typedef struct st_stats
 {
@@ -125,6 +128,13 @@ int64_t max_eigen_value_ex(void* wq, int dtype, const void* mat,
  * n, the number of rounds that did work (0 if the last solve was not
  * timed), or a negative value on error. */
 int st_last_round_times(void* wq, float* ms, unsigned int cap);
+
+/* Row sums of the last solve on this queue that ran with ST_FLAG_TRACE_SUMS:
+ * s_k for the evaluated rounds k = 0 .. n-1 (the vectors the stop test of
+ * similarity_transform.cpp:413-421 compared), copied as min(cap_rounds, n)
+ * rows of dim elements of the solve's dtype into `sums`.  Returns n (0 if the
+ * last solve was not traced) or a negative value on error. */
+int st_last_round_sums(void* wq, void* sums, unsigned int cap_rounds);
 
 /* Make the context launch on a caller stream (a hipStream_t; NULL is the
  * HIP null stream, which is torch's default stream).  Returns 0 or
@@ -294,6 +304,16 @@ int st_rowsum_f32(const float* d_mat, float* d_s, unsigned int nrows,
                   unsigned int ncols, void* stream);
 int st_rowsum_f64(const double* d_mat, double* d_s, unsigned int nrows,
                   unsigned int ncols, void* stream);
+/* The same row sums in the flat form, for blocks where st_round_flat_pays
+ * (what the solve loops run as their initial pass there): one short
+ * workgroup per (rows, column piece) writes partial sums into d_part
+ * (st_round_flat_scratch(nrows, ncols) elements), a second launch sums each
+ * row's pieces in a fixed order.  Deterministic and independent of the row
+ * partition among blocks of one cache class, like st_round_flat's sums. */
+int st_rowsum_flat_f32(const float* d_mat, float* d_s, float* d_part,
+                       unsigned int nrows, unsigned int ncols, void* stream);
+int st_rowsum_flat_f64(const double* d_mat, double* d_s, double* d_part,
+                       unsigned int nrows, unsigned int ncols, void* stream);
 
 /* Fused round body: for the local rows r in [0,nrows) (global row0 + r),
  *   A[r][c] = A[r][c] * ((1/s_cur[row0+r]) * s_cur[c])     (ST_SEM_SYCL)
@@ -442,10 +462,13 @@ int st_set_mfree_shape(unsigned int shape);
 #define ST_FORM_DEFER_READ 1  /* deferred writes: a read-only round          */
 #define ST_FORM_DEFER_STORE 2 /* deferred writes: the storing round          */
 #define ST_FORM_MFREE 3       /* the matrix-free round                        */
+#define ST_FORM_ROWSUM 4      /* K0, the initial row-sum pass                 */
 #define ST_KERNEL_ROUND 0     /* k_round: grid-stride row groups              */
 #define ST_KERNEL_FLAT 1      /* k_flat + k_parts, storing every round        */
 #define ST_KERNEL_FLAT_DEFERRED 2 /* k_flat<NP> + k_parts                     */
 #define ST_KERNEL_MFREE 3     /* k_mfree                                      */
+#define ST_KERNEL_FUSED 4     /* k_fused: grid-stride row groups, sums only    */
+#define ST_KERNEL_FLAT_SUM 5  /* k_flat_sum + k_parts                         */
 typedef struct st_launch_policy
 {
   int kernel;               /* ST_KERNEL_*                                    */

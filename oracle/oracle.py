@@ -75,6 +75,9 @@ def _declare(L: ctypes.CDLL) -> None:
         getattr(L, f"orc_similarity_transform_{sfx}").argtypes = [
             P, u32, T, u32, i32, i32, P, P, P, P, P, P]
         getattr(L, f"orc_similarity_transform_{sfx}").restype = i32
+        getattr(L, f"orc_similarity_transform_trace_{sfx}").argtypes = [
+            P, u32, T, u32, i32, i32, P, P, P, P, P, P, P]
+        getattr(L, f"orc_similarity_transform_trace_{sfx}").restype = i32
         getattr(L, f"orc_similarity_transform_gen_{sfx}").argtypes = [
             i32, u64, u32, T, u32, i32, i32, u32, P, P, P, P, P]
         getattr(L, f"orc_similarity_transform_gen_{sfx}").restype = i32
@@ -180,11 +183,15 @@ class Solve(NamedTuple):
     rounds_evaluated: int
     loop_ms: float
     max_dsum: np.ndarray   # per evaluated round, max |s_i - s_next| inspected
+    row_sums: Optional[np.ndarray] = None  # (rounds_evaluated, n) with trace=True
 
 
 def similarity_transform(mat: np.ndarray, semantics: int = SEM_SYCL, eps=None,
-                         max_itr: int = MAX_ITR, nthreads: int = 0) -> Solve:
-    """Whole solve (similarity_transform.cpp:5-75 or main.py:30-47)."""
+                         max_itr: int = MAX_ITR, nthreads: int = 0,
+                         trace: bool = False) -> Solve:
+    """Whole solve (similarity_transform.cpp:5-75 or main.py:30-47).
+    ``trace`` also returns every evaluated round's row sums s_k
+    (``row_sums``, the vectors the stop test compared)."""
     mat = np.ascontiguousarray(mat)
     if mat.dtype not in (np.float32, np.float64):
         mat = mat.astype(np.float64)
@@ -199,12 +206,19 @@ def similarity_transform(mat: np.ndarray, semantics: int = SEM_SYCL, eps=None,
     ev_n = np.zeros(1, dtype=np.uint32)
     ms = np.zeros(1, dtype=np.float64)
     dsum = np.zeros(max(max_itr, 1), dtype=np.float64)
-    rc = getattr(lib(), f"orc_similarity_transform_{sfx}")(
-        _ptr(mat), n, eps, max_itr, semantics, nthreads,
-        _ptr(ev), _ptr(vec), _ptr(it), _ptr(dsum), _ptr(ms), _ptr(ev_n))
+    args = (_ptr(mat), n, eps, max_itr, semantics, nthreads,
+            _ptr(ev), _ptr(vec), _ptr(it), _ptr(dsum), _ptr(ms), _ptr(ev_n))
+    sums = None
+    if trace:
+        sums = np.zeros((max(max_itr, 1), n), dtype=mat.dtype)
+        rc = getattr(lib(), f"orc_similarity_transform_trace_{sfx}")(*args, _ptr(sums))
+    else:
+        rc = getattr(lib(), f"orc_similarity_transform_{sfx}")(*args)
     if rc != 0:
         raise ValueError("oracle solve failed (bad arguments or out of memory)")
-    return Solve(ev[0], vec, int(it[0]), int(ev_n[0]), float(ms[0]), dsum[: int(ev_n[0])])
+    r = int(ev_n[0])
+    return Solve(ev[0], vec, int(it[0]), r, float(ms[0]), dsum[:r],
+                 None if sums is None else sums[:r])
 
 
 def max_threads() -> int:

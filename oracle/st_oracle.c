@@ -240,12 +240,12 @@ orc_now_ms(void)
  * rounds_evaluated: optional; number of row-sum evaluations performed.
  */
 #define DEFINE_SOLVE(T, SFX)                                                  \
-  int orc_similarity_transform_##SFX(const T* mat, uint32_t n, T eps,         \
-                                     uint32_t max_itr, int semantics,         \
-                                     int nthreads, T* eigen_val,              \
-                                     T* eigen_vec, uint32_t* iter_count,      \
-                                     double* max_dsum, double* loop_ms,       \
-                                     uint32_t* rounds_evaluated)              \
+  static int orc_solve_##SFX(const T* mat, uint32_t n, T eps,                 \
+                             uint32_t max_itr, int semantics, int nthreads,   \
+                             T* eigen_val, T* eigen_vec,                      \
+                             uint32_t* iter_count, double* max_dsum,          \
+                             double* loop_ms, uint32_t* rounds_evaluated,     \
+                             T* s_trace)                                      \
   {                                                                           \
     if (n == 0 || !mat || !eigen_val || !eigen_vec || !iter_count)            \
       return -1;                                                              \
@@ -269,6 +269,8 @@ orc_now_ms(void)
     for (; i < max_itr; i++) {                                                \
       orc_rowsum_##SFX(a, s, n, n);                                           \
       evals++;                                                                \
+      if (s_trace)                                                            \
+        memcpy(s_trace + (size_t)i * n, s, sizeof(T) * n);                    \
       T mx = orc_find_max_##SFX(s, n);                                        \
       orc_compute_eigen_vector_##SFX(s, mx, eigen_vec, n);                    \
       if (max_dsum) {                                                         \
@@ -295,6 +297,30 @@ orc_now_ms(void)
     free(a);                                                                  \
     free(s);                                                                  \
     return 0;                                                                 \
+  }                                                                           \
+  int orc_similarity_transform_##SFX(const T* mat, uint32_t n, T eps,         \
+                                     uint32_t max_itr, int semantics,         \
+                                     int nthreads, T* eigen_val,              \
+                                     T* eigen_vec, uint32_t* iter_count,      \
+                                     double* max_dsum, double* loop_ms,       \
+                                     uint32_t* rounds_evaluated)              \
+  {                                                                           \
+    return orc_solve_##SFX(mat, n, eps, max_itr, semantics, nthreads,         \
+                           eigen_val, eigen_vec, iter_count, max_dsum,        \
+                           loop_ms, rounds_evaluated, NULL);                  \
+  }                                                                           \
+  /* the same solve, also writing s_k of every evaluated round k into         \
+   * s_trace[k * n .. (k + 1) * n) ([max_itr * n]): the vectors the stop test  \
+   * compared, for checking a device solve's per-round decisions */           \
+  int orc_similarity_transform_trace_##SFX(                                   \
+    const T* mat, uint32_t n, T eps, uint32_t max_itr, int semantics,         \
+    int nthreads, T* eigen_val, T* eigen_vec, uint32_t* iter_count,           \
+    double* max_dsum, double* loop_ms, uint32_t* rounds_evaluated,            \
+    T* s_trace)                                                               \
+  {                                                                           \
+    return orc_solve_##SFX(mat, n, eps, max_itr, semantics, nthreads,         \
+                           eigen_val, eigen_vec, iter_count, max_dsum,        \
+                           loop_ms, rounds_evaluated, s_trace);               \
   }
 
 /*

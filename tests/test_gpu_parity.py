@@ -960,8 +960,14 @@ def test_fuzz_vs_oracle(eigen, orc):
     """Seeded random sweep over size, dtype, semantics, form, batch and
     eps: iteration counts equal to the oracle's, λ / v within the dtype's
     tolerance.  Sizes straddle the launch-shape switches (rows per group,
-    remainder groups, 16-byte vs element access)."""
+    remainder groups, 16-byte vs element access).  Every case runs traced on
+    both sides (tests/stop_parity.py): a count may differ only where the
+    two solves' own row sums put a round's max |Δs| on opposite sides of
+    eps, and that must be explained by their measured row-sum deviation
+    (at most DEV_ULPS ulps of max s)."""
+    import stop_parity as sp
     rng = np.random.default_rng(1234)
+    straddles = []
     for case in range(40):
         n = int(rng.choice([1, 2, 3, 7, 64, 127, 255, 1023, 1024, 1025, 2047, 2048, 2049,
                             2051, 3000]))
@@ -973,17 +979,68 @@ def test_fuzz_vs_oracle(eigen, orc):
         kind = "hilbert" if rng.random() < 0.5 else "random"
         mat = orc.hilbert(n, dt) if kind == "hilbert" else orc.random_matrix(n, case, dt)
         lam, v, ts, itr, st = eigen.similarity_transform_ex(
-            mat, eps=eps, semantics=sem, matrix_free=mf, batch=batch, max_itr=200)
-        ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=200)
+            mat, eps=eps, semantics=sem, matrix_free=mf, batch=batch, max_itr=200,
+            trace_sums=True)
+        ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=200, trace=True)
         tag = (case, n, dt.__name__, sem, mf, batch, eps, kind)
-        # a stop test within rounding of eps can legitimately flip in fp32
-        dmin = np.min(np.abs(ref.max_dsum - eps)) if len(ref.max_dsum) else 1.0
-        if dt == np.float32 and dmin < 1e-5 * max(1.0, float(np.max(mat.sum(1)))):
+        cmp = sp.compare(eigen.last_round_sums(), ref.row_sums, dt(eps),
+                         sem == _lib.ST_SEM_SYCL, 200)
+        if not sp.assert_stop_parity(cmp, tag):
+            straddles.append((tag, cmp["straddle"]))
             continue
         assert itr == ref.iter_count, tag
         tol = 1e-10 if dt == np.float64 else 2e-5
         assert abs(lam - ref.eigen_val) <= tol * abs(ref.eigen_val) + 1e-30, tag
         assert np.max(np.abs(v - ref.eigen_vec)) <= (1e-10 if dt == np.float64 else 5e-4), tag
+    assert len(straddles) <= 2, straddles
+
+
+@pytest.mark.parametrize("n", [512, 1024, 2048, 4096])
+def test_dropin_fp32_random_at_reference_eps(eigen, orc, n):
+    """The reference's wrapper test shape (wrapper/python/test.py:3-18: fp32
+    random matrices through max_eigen_value, EPS = 1e-3f from
+    include/similarity_transform.hpp:4, the cyclic stop of
+    similarity_transform.cpp:413-421) against the oracle: iteration count
+    equal, λ within 1e-5 relative, v within 1e-4, and the per-round stop
+    decisions traced on both sides (no round straddles EPS)."""
+    import stop_parity as sp
+    rng = np.random.default_rng(2021 + n)
+    mat = rng.random((n, n)).astype("f")          # wrapper/python/test.py:9
+    lam, v, ts, itr = eigen.similarity_transform(mat)            # the drop-in call
+    ref = orc.similarity_transform(mat, orc.SEM_SYCL, trace=True)
+    lam2, v2, _, itr2, st = eigen.similarity_transform_ex(mat, trace_sums=True)
+    assert lam2 == lam and itr2 == itr and np.array_equal(v2, v)  # tracing moves nothing
+    cmp = sp.compare(eigen.last_round_sums(), ref.row_sums, orc.EPS_F32, True, orc.MAX_ITR)
+    assert sp.assert_stop_parity(cmp, n), cmp
+    assert itr == ref.iter_count
+    assert abs(float(lam) - float(ref.eigen_val)) <= 1e-5 * float(ref.eigen_val)
+    assert np.max(np.abs(v.astype(np.float64) - ref.eigen_vec)) <= 1e-4
+    assert np.all(np.isclose(mat @ v, lam * v, atol=1e-3))       # the reference's own check
+
+
+def test_trace_sums_round_trip(eigen, solver, orc):
+    """ST_FLAG_TRACE_SUMS records s_0 .. s_{end-1} on every form (one-launch
+    round, flat deferred, matrix-free; drop-in and device paths) without
+    changing a result, and an untraced solve clears the trace."""
+    import stop_parity as sp
+    for n, dt, kw in ((300, np.float64, {}), (300, np.float32, dict(matrix_free=True)),
+                      (4352, np.float64, {}), (2048, np.float32, dict(matrix_free=True))):
+        mat = orc.hilbert(n, dt)
+        base = eigen.similarity_transform_ex(mat, **kw)
+        lam, v, _, itr, st = eigen.similarity_transform_ex(mat, trace_sums=True, **kw)
+        sums = eigen.last_round_sums()
+        assert lam == base[0] and itr == base[3] and np.array_equal(v, base[1])
+        assert sums.shape == (st["rounds"], n) and sums.dtype == dt
+        ref = orc.similarity_transform(mat, orc.SEM_SYCL, trace=True)
+        cmp = sp.compare(sums, ref.row_sums, dt(1e-3), True, orc.MAX_ITR)
+        assert sp.assert_stop_parity(cmp, n) and itr == ref.iter_count
+        t = torch.from_numpy(mat).to(DEV)
+        lam_d, v_d, it_d, st_d = solver.solve(t, trace_sums=True, **kw)
+        assert lam_d == lam and it_d == itr and np.array_equal(solver.last_round_sums(), sums)
+        eigen.similarity_transform_ex(mat, **kw)
+        assert eigen.last_round_sums().shape[0] == 0
+    with pytest.raises(ev.EigenValueError, match="TRACE_SUMS"):
+        eigen.similarity_transform_ex(orc.hilbert(4096), trace_sums=True, max_itr=100000)
 
 
 def test_config1_hilbert8192_fp64_vs_oracle(solver, orc):

@@ -32,7 +32,7 @@ BLOCKS = [
     ("f32", 32768, 32768, "configs[4]"),
 ]
 FORMS = [("round", 0, 0)] + [(f"read NP={k}", 1, k) for k in range(5)] + \
-    [("store NP=5", 2, 5), ("mfree", 3, 0)]
+    [("store NP=5", 2, 5), ("mfree", 3, 0), ("K0 rowsum", 4, 0)]
 
 
 def table():

@@ -1,0 +1,34 @@
+# round-6 GPU session steps (S=r06_sN STEPS="…" bash tools/session_r06.sh)
+set -u
+O=gpurun_out/${S:-r06_s1}; mkdir -p $O
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+fail() { echo "== stopping: $1 exited $2"; exit $2; }
+run() { # name secs cmd...  (rc 0/1 continue; anything else ends the session)
+  local n=$1 t=$2; shift 2
+  echo "== $n: $*"; local t0=$(date +%s)
+  timeout -k 10 $t "$@" > $O/$n.log 2>&1; local rc=$?
+  echo "== $n rc=$rc ($(( $(date +%s) - t0 ))s)"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then fail $n $rc; fi
+}
+for step in ${STEPS:-tests smoke bench}; do case $step in
+new)
+  # this round's new paths first (flat K0, traced solves): a failure ends the session
+  timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "rowsum or trace or fp32_random_at_reference_eps or fuzz or flat_round_vs_round or deferred_writes_bitwise or sharded_single_gpu or native_multi_gpu_flat" > $O/new.log 2>&1; rc=$?
+  tail -25 $O/new.log; [ $rc -eq 0 ] || fail new $rc ;;
+tests) run pytest_gpu 900 python3 -u -m pytest -x -q -rs --timeout 300 --timeout-method thread -m gpu tests/; tail -15 $O/pytest_gpu.log ;;
+smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -3 $O/smoke.log ;;
+fuzz) run fuzz 900 python3 -u tools/fuzz_parity.py --cases ${FUZZ_CASES:-300} --seed ${FUZZ_SEED:-20261201} --json $O/r06_fuzz_parity.json; tail -3 $O/fuzz.log; grep -c STRADDLE $O/fuzz.log ;;
+bench) run bench 900 python3 bench.py --steps 20 --warmup 5; tail -c 1500 $O/bench.log ;;
+benchquick) run benchquick 600 python3 bench.py --steps 20 --warmup 5 --no-cpu --no-north-star --no-headline; tail -c 2500 $O/benchquick.log ;;
+prof)
+  D=$O/prof; mkdir -p $D
+  run prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-north-star --no-headline
+  head -14 $D/run_kernel_stats.csv ;;
+k0)
+  # K0 (the initial row-sum pass) alone at configs[1] and the north star,
+  # both forms, under a kernel trace
+  D=$O/k0; mkdir -p $D
+  run k0 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/k0_probe.py
+  cat $O/k0.log | tail -12; head -12 $D/run_kernel_stats.csv ;;
+*) echo "unknown step $step"; exit 2 ;;
+esac; done
