@@ -2,23 +2,39 @@
 # Usage: make [-j16]      (the same recipe __graft_entry__.build() runs)
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
+# -fvisibility=hidden: the dynamic ABI is exactly what include/*.h declares
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
-            -fno-fast-math -Wall -Wextra -Wno-unused-parameter -Iinclude \
-            -Ieigen_value_amd/csrc
+            -fno-fast-math -fvisibility=hidden -fvisibility-inlines-hidden \
+            -Wall -Wextra -Wno-unused-parameter -Iinclude -Ieigen_value_amd/csrc
 SRC      := eigen_value_amd/csrc/st_kernels.hip eigen_value_amd/csrc/st_solve.hip \
             eigen_value_amd/csrc/st_multi.hip eigen_value_amd/csrc/st_rendezvous.hip
 OBJ      := $(patsubst eigen_value_amd/csrc/%.hip,build/%.o,$(SRC))
 LIB      := eigen_value_amd/lib/libsimilarity_transform.so
+# the tuning build (tools and the knob tests only): the same objects, with
+# st_kernels compiled to also export the launch-table setters of
+# include/st_tuning.h
+TUNING_OBJ := build/st_kernels_tuning.o $(filter-out build/st_kernels.o,$(OBJ))
+LIB_TUNING := eigen_value_amd/lib/libsimilarity_transform_tuning.so
+HDRS     := include/similarity_transform.h include/st_tuning.h eigen_value_amd/csrc/st_internal.h \
+            eigen_value_amd/csrc/st_device.h eigen_value_amd/csrc/st_rendezvous.h
 
-all: $(LIB) oracle
+all: $(LIB) $(LIB_TUNING) oracle
 
-build/%.o: eigen_value_amd/csrc/%.hip include/similarity_transform.h eigen_value_amd/csrc/st_internal.h eigen_value_amd/csrc/st_device.h eigen_value_amd/csrc/st_rendezvous.h
+build/%.o: eigen_value_amd/csrc/%.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+build/st_kernels_tuning.o: eigen_value_amd/csrc/st_kernels.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -DST_TUNING_ABI=1 -c $< -o $@
 
 $(LIB): $(OBJ)
 	@mkdir -p eigen_value_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
+$(LIB_TUNING): $(TUNING_OBJ)
+	@mkdir -p eigen_value_amd/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(TUNING_OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 oracle:
 	$(MAKE) -C oracle

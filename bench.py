@@ -444,8 +444,7 @@ def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     brackets each launch with its own pair for the kernel average."""
     cool_down(torch)
     sh.start()
-    for _ in range(warmup):
-        sh.round(0.0, BIG)
+    sh.rounds(warmup, 0.0, BIG)
     torch.cuda.synchronize()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))]
     if world > 1:
@@ -456,8 +455,9 @@ def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     t0 = time.perf_counter()
     if world == 1:
         ev[0][0].record()
-    for _ in range(steps):
-        sh.round(0.0, BIG)
+    # the K rounds through pre-resolved launches (sh.rounds: round()'s
+    # kernels, arguments and all-gather, without its per-call Python work)
+    sh.rounds(steps, 0.0, BIG)
     if world == 1:
         ev[0][1].record()
     torch.cuda.synchronize()
@@ -1055,17 +1055,22 @@ def stall_test(args, dist):
     the watchdog, the spawning parent's deadline and the communicator
     rendezvous can be tested without a GPU.  --stall-in barrier: the others
     wait in a barrier (a rank stuck in a collective); --stall-in rendezvous:
-    they make the library communicator's pre-RCCL presence check
-    (sharded.rendezvous), which names rank R within --comm-timeout."""
+    they take the library communicator as a sharded solve does
+    (make_comm_agreed over RcclComm: the id hand-over, then st_comm_init's
+    pre-RCCL rendezvous), which names rank R within --comm-timeout."""
     dist.init_process_group("gloo")
     progress("stall test: process group up")
     if dist.get_rank() == args.stall_rank:
         progress("stall test: this rank sleeps")
         time.sleep(10 ** 6)
     if args.stall_in == "rendezvous":
-        from eigen_value_amd import sharded
+        from eigen_value_amd import _lib, sharded
+        _lib.load().st_set_comm_timeout(args.comm_timeout)
         try:
-            sharded.rendezvous(None, args.comm_timeout)
+            comm, _ = sharded.make_comm_agreed(
+                None, lambda: sharded.RcclComm(None, device_index=0, timeout=args.comm_timeout))
+            if comm is not None:
+                comm.close()
         except sharded.PeerMissingError as e:
             print(f"bench.py: rank {dist.get_rank()}: {e}", file=sys.stderr, flush=True)
             raise SystemExit(3) from None   # no RCCL state exists: a normal exit

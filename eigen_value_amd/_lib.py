@@ -13,7 +13,11 @@ from typing import Optional
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 DEFAULT_LIB = os.path.join(PKG_DIR, "lib", "libsimilarity_transform.so")
+# the tuning build: the same kernels plus the launch-table setters of
+# include/st_tuning.h (tools and the knob tests only)
+TUNING_LIB = os.path.join(PKG_DIR, "lib", "libsimilarity_transform_tuning.so")
 HEADER = os.path.join(REPO_DIR, "include", "similarity_transform.h")
+TUNING_HEADER = os.path.join(REPO_DIR, "include", "st_tuning.h")
 
 ST_SEM_SYCL = 0
 ST_SEM_MAINPY = 1
@@ -124,10 +128,49 @@ def load(path: Optional[str] = None) -> ctypes.CDLL:
     if L is None:
         L = ctypes.CDLL(p)
         _declare(L)
+        if hasattr(L, "st_set_defer_caps"):     # the tuning build
+            declare_tuning(L)
         _by_path[key] = L
     if path is None:
         _lib = L
     return L
+
+
+def load_tuning() -> ctypes.CDLL:
+    """The tuning build (libsimilarity_transform_tuning.so), declared with
+    the main ABI and the setters of include/st_tuning.h.  A separate library
+    with its own launch tables: a knob set here moves only the launches made
+    through it (run a knob study with EIGEN_VALUE_LIB pointing at it, so
+    that the package's default library is this one)."""
+    L = load(TUNING_LIB)
+    declare_tuning(L)
+    return L
+
+
+def declare_tuning(L: ctypes.CDLL) -> None:
+    """argtypes of the st_tuning.h setters (raises AttributeError on the
+    product library, which exports none)."""
+    u32, i32 = ctypes.c_uint32, ctypes.c_int
+    L.st_set_flat_grid_limit.argtypes = [u32]
+    L.st_set_flat_grid_limit.restype = u32
+    L.st_set_defer_caps.argtypes = [i32, i32, u32, u32]
+    L.st_set_defer_caps.restype = i32
+    L.st_set_defer_ntload.argtypes = [u32, u32]
+    L.st_set_defer_ntload.restype = i32
+    L.st_defer_ntload_class.argtypes = [u32, u32, i32]
+    L.st_defer_ntload_class.restype = i32
+    L.st_set_every_cache.argtypes = [u32, u32]
+    L.st_set_every_cache.restype = i32
+    L.st_every_cache_class.argtypes = [u32, u32, i32]
+    L.st_every_cache_class.restype = i32
+    L.st_set_every_tile.argtypes = [u32, u32]
+    L.st_set_every_tile.restype = i32
+    L.st_set_every_caps.argtypes = [u32, u32]
+    L.st_set_every_caps.restype = i32
+    L.st_set_defer_cache.argtypes = [i32, u32, u32]
+    L.st_set_defer_cache.restype = i32
+    L.st_set_mfree_shape.argtypes = [u32]
+    L.st_set_mfree_shape.restype = i32
 
 
 def _declare(L: ctypes.CDLL) -> None:
@@ -202,32 +245,14 @@ def _declare(L: ctypes.CDLL) -> None:
     L.st_round_flat_pays.restype = i32
     L.st_defer_rounds.argtypes = [u32, u32, i32]
     L.st_defer_rounds.restype = u32
-    L.st_set_flat_grid_limit.argtypes = [u32]
-    L.st_set_flat_grid_limit.restype = u32
-    L.st_set_defer_caps.argtypes = [i32, i32, u32, u32]
-    L.st_set_defer_caps.restype = i32
-    L.st_set_defer_ntload.argtypes = [u32, u32]
-    L.st_set_defer_ntload.restype = i32
-    L.st_defer_ntload_class.argtypes = [u32, u32, i32]
-    L.st_defer_ntload_class.restype = i32
-    L.st_set_every_cache.argtypes = [u32, u32]
-    L.st_set_every_cache.restype = i32
-    L.st_every_cache_class.argtypes = [u32, u32, i32]
-    L.st_set_every_tile.argtypes = [u32, u32]
-    L.st_set_every_caps.argtypes = [u32, u32]
-    L.st_set_every_caps.restype = i32
-    L.st_set_defer_cache.argtypes = [i32, u32, u32]
-    L.st_set_mfree_shape.argtypes = [u32]
-    L.st_set_mfree_shape.restype = i32
-    L.st_set_defer_cache.restype = i32
-    L.st_set_every_tile.restype = i32
-    L.st_every_cache_class.restype = i32
     L.st_comm_unique_id.argtypes = [ctypes.c_char_p]
     L.st_comm_unique_id.restype = i32
     L.st_comm_unique_id_addr.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
     L.st_comm_unique_id_addr.restype = i32
     L.st_comm_init.argtypes = [ctypes.POINTER(ctypes.c_void_p), i32, i32, ctypes.c_char_p, i32]
     L.st_comm_init.restype = i32
+    L.st_comm_id_release.argtypes = [ctypes.c_char_p]
+    L.st_comm_id_release.restype = i32
     L.st_comm_destroy.argtypes = [P]
     L.st_comm_destroy.restype = i32
     L.st_set_comm_timeout.argtypes = [ctypes.c_double]
@@ -290,6 +315,7 @@ def declared_symbols(header: str = HEADER) -> list[str]:
     import re
     text = open(header).read()
     body = text.split('extern "C" {', 1)[1].split('} /* extern "C" */', 1)[0]
+    body = body.split("#ifdef __cplusplus", 1)[0]
     body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
     names = re.findall(r"\b([A-Za-z_][A-Za-z0-9_]*)\s*\(", body)
     skip = {"sizeof"}

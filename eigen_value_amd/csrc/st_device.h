@@ -242,16 +242,6 @@ ld(const V* p)
 // profiles/r02_flat_map_rowload_*.log): 15-30 % SLOWER on non-temporal
 // fp64 blocks with pending rounds (32768^2, NP = 1: 1.62 vs 1.33 ms), equal
 // elsewhere, so the library keeps scalar row loads.
-// Probe-only forms of k_flat, compiled only into the tools' sweep builds
-// (tools/Makefile passes -DST_PROBE_FORMS=1): FOLD (k_parts folded into the
-// last arriving workgroup of a row group), DS = -1 with pending rounds (the
-// store decided at run time), FlatPending::pc (pieces walked in column
-// blocks) and the gates other than kGatePlain.  The library launches none of
-// them; k_flat refuses them at compile time without the switch.
-#ifndef ST_PROBE_FORMS
-#define ST_PROBE_FORMS 0
-#endif
-
 #ifndef ST_ROW_VLOAD
 #define ST_ROW_VLOAD 0
 #endif
@@ -895,37 +885,19 @@ flat_nblocks(uint32_t nrows, uint32_t ncols, uint32_t ppr, uint32_t col0,
 
 // How a flat workgroup learns that its launch follows the stopping round
 // (state->end != 0 && end <= k).  Millions of short workgroups each pay
-// this, so its latency matters (a persistent kernel pays it once per CU):
-//   kGateAtomic   agent-scope atomic load (an L2 round trip) before any
-//                 matrix load is issued
-//   kGatePlain    plain load, served from the CU's L1 after the first
-//                 workgroup of the launch on that CU.  Exact: `end` only
-//                 changes inside the stopping launch k (to k + 1, which
-//                 gates nothing in launch k), and every launch starts with
-//                 the L1 invalidated
-//   kGateNone     no gate (sweep ceiling only; not a valid solve)
-//   kGateSpec     the matrix loads are issued first and the atomic gate is
-//                 read while they are in flight; a gated launch then reads
-//                 but never writes
-// The plain load compiles to a scalar load (uniform address, nothing stored
-// before it); it times like no gate at all and 1.8 % faster than the atomic
-// gate per round at 32768^2 fp64, 3.5 % on the P = 8 row block, within
-// -0.7 % (8192^2 fp64) ... +3.5 % elsewhere
-// (profiles/r01_sweep_gate*.log, SWEEP_GATE=1 tools/sweep_dir), so the
-// library launches k_flat with it.
-enum { kGateAtomic = 0, kGatePlain = 1, kGateNone = 2, kGateSpec = 3 };
-
-template <int GATE>
+// this, so its latency matters: a plain load, served from the CU's L1 after
+// the first workgroup of the launch on that CU.  Exact: `end` only changes
+// inside the stopping launch k (to k + 1, which gates nothing in launch k),
+// and every launch starts with the L1 invalidated.  It compiles to a scalar
+// load (uniform address, nothing stored before it) and times like no gate
+// at all: 1.8 % faster than an agent-scope atomic load per round at 32768^2
+// fp64, 3.5 % on the P = 8 row block, within -0.7 % (8192^2) ... +3.5 %
+// elsewhere (profiles/r01_sweep_gate*.log; the round-1 sweep tool's atomic,
+// speculative and no-gate forms are in the git history).
 __device__ __forceinline__ bool
 flat_gated(const st_state* state, uint32_t k)
 {
-  uint32_t e;
-  if constexpr (GATE == kGateNone)
-    return false;
-  else if constexpr (GATE == kGatePlain)
-    e = state->end; // not volatile: volatile bypasses the L1 (sc0 sc1)
-  else
-    e = __hip_atomic_load(&state->end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t e = state->end; // not volatile: volatile bypasses the L1 (sc0 sc1)
   return e != 0 && e <= k;
 }
 
@@ -965,31 +937,22 @@ struct FlatPending
   const T* s[NP > 0 ? NP : 1];
   const T* inv[NP > 0 ? NP : 1];
   const T* inv_cur; // 1 / s_k (the current round's row scales)
-  uint32_t store;   // store A_{k+1} this round
   uint32_t pt;      // piece-tiled workgroup order: pt row groups of a piece
                     // back to back (0 = row-major; see k_flat)
-  uint32_t pc;      // with pt: the pieces walked in column blocks of pc
-                    // pieces, each tiled as a block of its own (0 = one
-                    // column block; long rows, see k_flat)
 };
 
-template <typename T, int W, int ORDER, bool NT, int R = 1, bool PW = false,
-          bool FS = false, int ALT = 0, int BLK = kBlock, int SPLIT = 0,
-          int GATE = kGatePlain, int NP = -1, int U = 1, bool FOLD = false,
-          int DS = -1, bool MF = false, int FLIP = 0>
-__global__ __launch_bounds__(BLK) void
+template <typename T, int W, int ORDER, bool NT, int R = 1, bool FS = false,
+          int ALT = 0, int SPLIT = 0, int NP = -1, int U = 1, int DS = -1,
+          bool MF = false, int FLIP = 0>
+__global__ __launch_bounds__(kBlock) void
 k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        T* __restrict__ v, uint32_t nrows, uint32_t ncols, uint32_t ppr,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
-       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0,
-       T* __restrict__ s_next = nullptr, uint32_t* __restrict__ fold_cnt = nullptr)
+       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0)
 {
-  // FOLD (sweep probe, SWEEP_FOLD=1 tools/sweep_dir): the last of a row
-  // group's ppr workgroups to finish sums the group's partials into s_next
-  // (k_parts' order, no v update) instead of a k_parts launch; fold_cnt[rg]
-  // counts arrivals and is reset by the last one
+  constexpr int BLK = kBlock;
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
   // columns [col0, col1) whose scales this rank computed itself, over the
   // ppr pieces starting at piece p_lo (no stats, no v update); 2 = every
@@ -1001,15 +964,13 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // s_k) also fold m_k / stop_k into the state (stats_publish); the v update
   // then moves to k_parts, after m_k is known
   // R rows of one column piece per workgroup (the piece's column scales are
-  // loaded once for the R rows); PW: one partial per wave instead of a
-  // workgroup combine (no barrier before the workgroup retires)
+  // loaded once for the R rows)
   // U: chunks of BLK * W columns per piece, chunk u of a lane BLK * W
   // columns after chunk u - 1 (the element-wide path, W = 1, takes U =
   // 16 / sizeof(T) so that its pieces hold as many bytes as the vector
   // path's)
-  // DS (deferred rounds): whether the launch stores A_{k+1}, fixed at
-  // compile time (1 / 0; the library's launches), or -1 = pend.store at
-  // run time (the sweep tools)
+  // DS (deferred rounds, NP >= 0): whether the launch stores A_{k+1}, fixed
+  // at compile time (1 / 0)
   // FLIP: the launch's cache policy (g_every_cache / g_defer_flip in
   // st_kernels.hip): bit 0 turns the matrix loads' policy over (cached <->
   // non-temporal), bit 1 the stores'; the shapes stay the form's
@@ -1018,16 +979,13 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // sum is Σ_c A_0[r][c] x[c] with x = v_{k-2} ∘ s_{k-1}, the first row
   // group folds round k-1's stats, nothing is stored; k_mparts finishes
   // s_k and v_{k-1}
-  static_assert(!MF || (FS && NP < 0 && SPLIT == 0 && GATE != kGateSpec),
+  static_assert(!MF || (FS && NP < 0 && SPLIT == 0),
                 "MF: the fused-stats unsplit round (gated on k - 1)");
-  static_assert(ST_PROBE_FORMS || (!FOLD && (NP < 0 || DS >= 0) && GATE == kGatePlain),
-                "probe-only k_flat form: tools builds only (-DST_PROBE_FORMS=1)");
+  static_assert(NP < 0 || DS >= 0, "a deferred round's store is decided at compile time");
   // the matrix-free launch k evaluates round k - 1 (gated once end <= k - 1)
   const uint32_t kr = MF ? k - 1 : k;
-  if constexpr (GATE != kGateSpec) {
-    if (flat_gated<GATE>(state, kr))
-      return;
-  }
+  if (flat_gated(state, kr))
+    return;
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
   constexpr uint32_t PWC = (uint32_t)BLK * W * U; // columns per piece
@@ -1068,21 +1026,11 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
     // piece's column scales - s_k and the pending rounds' - in its L1
     // instead of refetching them from L2 (deferred rounds; and the
     // every-round launch on non-temporal blocks, tiles of 4)
-    // With pc (long rows): the pieces in column blocks of pc, the whole
-    // block's row groups tiled over one column block before the next
     const uint32_t pt = pend.pt, ng = (nrows + R - 1) / R;
-    uint32_t bb = b, w = ppr, pb = 0;
-    if (ST_PROBE_FORMS && pend.pc != 0 && pend.pc < ppr) { // uniform
-      const uint32_t cb = b / (ng * pend.pc);
-      pb = cb * pend.pc;
-      bb = b - cb * (ng * pend.pc);
-      w = ppr - pb < pend.pc ? ppr - pb : pend.pc;
-    }
-    const uint32_t tile = bb / (pt * w), t = bb - tile * (pt * w);
+    const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);
     const uint32_t left = ng - tile * pt, g = left < pt ? left : pt;
     p = t / g;
     rg = tile * pt + (t - p * g);
-    p += pb;
   } else {
     rg = b / ppr;
     p = b - rg * ppr;
@@ -1108,7 +1056,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // fp64; the every-round and NP = 0 forms lose up to 3 %,
   // profiles/r02_flat_map_ab_*.log)
   constexpr bool UM = SPLIT == 0 && NP > 0 && ST_FLAT_UNMASKED;
-  const bool do_store = NP < 0 || (DS >= 0 ? DS == 1 : pend.store != 0); // uniform
+  constexpr bool do_store = NP < 0 || DS == 1;
   // the deferred rounds' stores (probe switch ST_DEFER_STORE_NT: non-temporal
   // on cached blocks too)
   constexpr bool NTS = (NT || (NP >= 0 && ST_DEFER_STORE_NT)) != ((FLIP & 2) != 0);
@@ -1203,10 +1151,6 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
           sp_r[i][j] = r0 + j < nrows ? ld_row(pend.inv[i] + row0 + r0 + j) : (T)1;
       }
     }
-  }
-  if constexpr (GATE == kGateSpec) {
-    if (flat_gated<kGateAtomic>(state, k))
-      return;
   }
   if constexpr (FS) {
     if (rg == 0) { // uniform per workgroup
@@ -1324,72 +1268,21 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 #pragma unroll
   for (int j = 0; j + 1 < R; j += 2) {
     const T t = wave_sum_pair(acc[j], acc[j + 1]);
-    if (lane >= 62) {
-      const uint32_t jj = j + (lane - 62);
-      if constexpr (PW) {
-        if (r0 + jj < nrows)
-          part[((size_t)(r0 + jj) * ppr + p) * NW + wave] = t;
-      } else {
-        red[wave][jj] = t;
-      }
-    }
+    if (lane >= 62)
+      red[wave][j + (lane - 62)] = t;
   }
   if constexpr (R % 2 == 1) {
     const T t = wave_sum_l63(acc[R - 1]);
-    if (lane == 63) {
-      if constexpr (PW) {
-        if (r0 + R - 1 < nrows)
-          part[((size_t)(r0 + R - 1) * ppr + p) * NW + wave] = t;
-      } else {
-        red[wave][R - 1] = t;
-      }
-    }
+    if (lane == 63)
+      red[wave][R - 1] = t;
   }
-  if constexpr (!PW) {
-    __syncthreads();
-    if (threadIdx.x < R && r0 + threadIdx.x < nrows) {
-      T t = red[0][threadIdx.x];
+  __syncthreads();
+  if (threadIdx.x < R && r0 + threadIdx.x < nrows) {
+    T t = red[0][threadIdx.x];
 #pragma unroll
-      for (int w = 1; w < NW; w++)
-        t += red[w][threadIdx.x];
-      if constexpr (FOLD) {
-        // an agent-scope atomic store (past the per-XCD L2s), completed
-        // before the arrival below (wave 0 waits on its memory counter)
-        __hip_atomic_store(&part[(size_t)(r0 + threadIdx.x) * ppr + p], t,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
-      }
-    }
-    if constexpr (FOLD) {
-      if (wave == 0) {
-        // wave 0 wrote the partials: release them, count the arrival
-        uint32_t before = 0;
-        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane == 0) {
-          before = __hip_atomic_fetch_add(&fold_cnt[rg], 1u, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-        }
-        before = __shfl(before, 0);
-        if (before == ppr - 1) {
-#pragma unroll
-          for (int j = 0; j < R; j++) {
-            if (r0 + j < nrows) {
-              const T* row = part + (size_t)(r0 + j) * ppr;
-              T acc2 = (T)0;
-              for (uint32_t q = lane; q < ppr; q += 64)
-                acc2 += __hip_atomic_load(&row[q], __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-              acc2 = wave_sum(acc2);
-              if (lane == 0)
-                s_next[r0 + j] = acc2;
-            }
-          }
-          if (lane == 0)
-            fold_cnt[rg] = 0u;
-        }
-      }
-    }
+    for (int w = 1; w < NW; w++)
+      t += red[w][threadIdx.x];
+    part[(size_t)(r0 + threadIdx.x) * ppr + p] = t;
   }
 }
 
@@ -1485,37 +1378,6 @@ k_state_mirror(const uint32_t* __restrict__ d, uint32_t* h)
   const uint32_t i = threadIdx.x;
   if (i < (uint32_t)(sizeof(st_state) / 4))
     __hip_atomic_store(&h[i], d[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// k_parts with one THREAD per row (sweep variant): the row's partials in
-// four interleaved running sums, ((a0 + a1) + (a2 + a3)), no wave reduction
-template <typename T, int BLK = kBlock>
-__global__ __launch_bounds__(BLK) void
-k_parts_t(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
-          uint32_t ppr, uint32_t k, const st_state* state,
-          const T* __restrict__ s_cur = nullptr, T* __restrict__ v = nullptr,
-          uint32_t row0 = 0)
-{
-  if (flat_gated<kGatePlain>(state, k))
-    return;
-  const uint32_t r = blockIdx.x * BLK + threadIdx.x;
-  if (r >= nrows)
-    return;
-  const T* row = part + (size_t)r * ppr;
-  T a[4] = { (T)0, (T)0, (T)0, (T)0 };
-  uint32_t p = 0;
-  for (; p + 4 <= ppr; p += 4) {
-#pragma unroll
-    for (int j = 0; j < 4; j++)
-      a[j] += row[p + j];
-  }
-  for (int j = 0; p < ppr; p++, j++)
-    a[j] += row[p];
-  s_next[r] = (a[0] + a[1]) + (a[2] + a[3]);
-  if (v != nullptr) {
-    const T m = (T)state->max;
-    v[row0 + r] = v[row0 + r] * (s_cur[row0 + r] / m);
-  }
 }
 
 // The matrix-free round's second launch (after k_flat<..., MF>): one wave

@@ -19,6 +19,13 @@
 #include "st_device.h"
 #include "st_internal.h"
 
+#ifndef ST_TUNING_ABI
+#define ST_TUNING_ABI 0
+#endif
+#if ST_TUNING_ABI
+#include "st_tuning.h"
+#endif
+
 // A/B probe switches of the launch shapes (st_device.h has those of the
 // kernel code: ST_DPP_NOINIT, ST_ROW_VLOAD, ST_FLAT_UNMASKED,
 // ST_DEFER_STORE_NT).  Probe builds of the library
@@ -635,8 +642,7 @@ launch_mfree_flat_cfg(const T* a0, const T* s_prev, T* s_next, const T* v_prev, 
   dev::FlatPending<T, -1> pe{};
   pe.pt = 8u;
   const uint32_t lds = defer_cap_lds(NT ? 5u : 4u);
-  hipLaunchKernelGGL((dev::k_flat<T, W, 0, NT, R, false, true, kFlatAlt, kBlock, 0,
-                                  dev::kGatePlain, -1, U, false, -1, true>),
+  hipLaunchKernelGGL((dev::k_flat<T, W, 0, NT, R, true, kFlatAlt, 0, -1, U, -1, true>),
                      fg.grid, dim3(kBlock), lds, stream, const_cast<T*>(a0), s_prev, part,
                      const_cast<T*>(v_prev), nrows, ncols, ppr, row0, k, st, eps, max_itr,
                      semantics, 0u, 0u, 0u, pe, fg.gx2);
@@ -788,8 +794,8 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
         std::memory_order_relaxed));
 #define ST_EVERY(FL)                                                           \
   hipLaunchKernelGGL(                                                          \
-    (dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt, kBlock, 0,         \
-                 dev::kGatePlain, -1, U, false, -1, false, FL>),               \
+    (dev::k_flat<T, W, ORDER, NT, R, true, kFlatAlt, 0, -1, U, -1, false,      \
+                 FL>),                                                         \
     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v, nrows, ncols, ppr,  \
     row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
     constexpr int kV = W > 1 ? 1 : 0;
@@ -807,8 +813,7 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     hipLaunchKernelGGL((dev::k_stats<T>), dim3(sgrid), dim3(kBlock), 0, stream,
                        s_cur, ncols, eps, k, max_itr, semantics, st);
     hipLaunchKernelGGL(
-      (dev::k_flat<T, W, ORDER, NT, R, false, false, kFlatAlt, kBlock, 0,
-                   dev::kGatePlain, -1, U>),
+      (dev::k_flat<T, W, ORDER, NT, R, false, kFlatAlt, 0, -1, U>),
       fg.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
       row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2);
     hipLaunchKernelGGL((dev::k_parts<T>), dim3(pgrid), dim3(kBlock), 0, stream,
@@ -889,13 +894,11 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
     pd.inv[i] = pend_inv[i];
   }
   pd.inv_cur = inv_cur;
-  pd.store = STORE ? 1u : 0u;
   pd.pt = pt;
   const FlatGrid fg = flat_grid(grid);
   // lds: dynamic LDS the kernel does not use, reserved only to cap the
   // workgroups per CU (see launch_flat_deferred)
-  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, false, true, kFlatAlt,
-                                  kBlock, 0, dev::kGatePlain, NP, U, false,
+  hipLaunchKernelGGL((dev::k_flat<T, W, ORDER, NT, R, true, kFlatAlt, 0, NP, U,
                                   STORE ? 1 : 0, false, FL>),
                      fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v,
                      nrows, ncols, ppr, row0, k, st, eps, max_itr, semantics,
@@ -967,7 +970,7 @@ std::atomic<uint32_t> g_defer_caps[2][2][7] = {
 // (32768^2 fp64 0x1 / 0x3 / 0x1f 1.499 / 1.523 / 1.617 vs 1.481 ms, 0x40 /
 // 0x80 1.478 / 1.485; fp32 0.739 - 0.758 vs 0.729; the P = 8 block 0.769 /
 // 0.827 vs 0.760), so it keeps both non-temporal.
-constexpr int kNtLoadClasses = 3;               // st_set_defer_ntload: fp64, cached
+[[maybe_unused]] constexpr int kNtLoadClasses = 3; // st_set_defer_ntload: fp64, cached
 constexpr int kDeferFlipClasses = 4;
 std::atomic<uint32_t> g_defer_flip[2][kDeferFlipClasses] = {
   { 0u, 0x41u, 0x41u, 0u },      // fp32
@@ -975,7 +978,7 @@ std::atomic<uint32_t> g_defer_flip[2][kDeferFlipClasses] = {
 };
 // bit 7: the storing round's stores turned over too
 constexpr uint32_t kNtStoreBit = 7u;
-constexpr uint32_t kNtLoadMask = 0xdfu;
+[[maybe_unused]] constexpr uint32_t kNtLoadMask = 0xdfu;
 
 // below 384 MiB, below 640 MiB, above (the cached fp64 classes of
 // st_set_defer_ntload)
@@ -1266,15 +1269,13 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
     // about to re-read (profiles/r01_split_cost.log)
     if (NT || col1 - col0 < ncols)
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, false, kFlatAlt, kBlock, 1,
-                     dev::kGatePlain, -1, U>),
+        (dev::k_flat<T, W, ORDER, true, kFlatRows, false, kFlatAlt, 1, -1, U>),
         fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
         npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
         dev::FlatPending<T, -1>{}, fl.gx2);
     else
       hipLaunchKernelGGL(
-        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, false, kFlatAlt, kBlock, 1,
-                     dev::kGatePlain, -1, U>),
+        (dev::k_flat<T, W, ORDER, false, kFlatRows, false, kFlatAlt, 1, -1, U>),
         fl.grid, dim3(kBlock), 0, stream, a, s_cur, part_local, v, nrows, ncols,
         npl, row0, k, st, eps, max_itr, semantics, p_lo, col0, col1,
         dev::FlatPending<T, -1>{}, fl.gx2);
@@ -1286,8 +1287,7 @@ launch_split_flat_cfg(int span, T* a, const T* s_cur, T* s_next, T* part,
   dev::split_full_pieces<PW>(ncols, ppr, col0, col1, pa, nfull);
   const FlatGrid fr = flat_grid(ppr + (ngroups - 1) * (ppr - nfull));
   hipLaunchKernelGGL(
-    (dev::k_flat<T, W, ORDER, NT, kFlatRows, false, true, kFlatAlt, kBlock, 2,
-                 dev::kGatePlain, -1, U>),
+    (dev::k_flat<T, W, ORDER, NT, kFlatRows, true, kFlatAlt, 2, -1, U>),
     fr.grid, dim3(kBlock), 0, stream, a, s_cur, part, v, nrows, ncols, ppr,
     row0, k, st, eps, max_itr, semantics, 0u, col0, col1,
     dev::FlatPending<T, -1>{}, fr.gx2);
@@ -1952,6 +1952,10 @@ st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype)
   return st::round_flat_pays(nrows, ncols, dtype == 1 ? 8 : 4) ? 1 : 0;
 }
 
+// ---- tuning setters (include/st_tuning.h): the tuning build only -------
+// (libsimilarity_transform_tuning.so, -DST_TUNING_ABI=1; the library the
+// drop-in callers load exports none of them)
+#if ST_TUNING_ABI
 int
 st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
                   unsigned int wg_per_cu)
@@ -2073,5 +2077,7 @@ st_set_flat_grid_limit(unsigned int max_x)
   st::g_flat_grid_x.store(gx, std::memory_order_relaxed);
   return gx;
 }
+
+#endif // ST_TUNING_ABI
 
 } // extern "C"

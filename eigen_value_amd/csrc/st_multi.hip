@@ -220,6 +220,11 @@ init_with_deadline(const std::shared_ptr<InitJob>& job,
       while (!job->done.load(std::memory_order_acquire) && elapsed() < t_c + 2.0)
         std::this_thread::sleep_for(std::chrono::milliseconds(1));
       const bool stuck = !job->done.load(std::memory_order_acquire);
+      // the helper may have finished with a live communicator just before
+      // it could see the cancel (it read gave_up == false first): that init
+      // succeeded, late, and the communicator is the caller's
+      if (!stuck && job->r == ncclSuccess)
+        return 0;
       ::st::set_error(
         "%s: %s still in progress after %.1f s (deadline %.1f s, "
         "ST_COMM_TIMEOUT_S / st_set_comm_timeout): a peer stopped after the "
@@ -760,7 +765,8 @@ st_comm_unique_id(char* id_out /* ST_COMM_ID_BYTES */)
 {
   st::clear_error();
   ST_REQUIRE(id_out, "st_comm_unique_id: null output");
-  return st::rdv_make_id(id_out); // st_rendezvous.hip
+  // st_rendezvous.hip; an id never joined is reaped after two deadlines
+  return st::rdv_make_id(id_out, nullptr, 2.0 * st::comm_timeout_s() + 30.0);
 }
 
 int
@@ -768,7 +774,15 @@ st_comm_unique_id_addr(char* id_out, const char* addr)
 {
   st::clear_error();
   ST_REQUIRE(id_out, "st_comm_unique_id_addr: null output");
-  return st::rdv_make_id(id_out, addr);
+  return st::rdv_make_id(id_out, addr, 2.0 * st::comm_timeout_s() + 30.0);
+}
+
+int
+st_comm_id_release(const char* id)
+{
+  st::clear_error();
+  ST_REQUIRE(id, "st_comm_id_release: null id");
+  return st::rdv_release(id);
 }
 
 int

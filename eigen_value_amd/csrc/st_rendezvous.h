@@ -8,9 +8,15 @@ namespace st {
 constexpr int kRdvIdBytes = 128;      // st_comm_unique_id's id
 constexpr int kRdvPayloadBytes = 128; // what the host hands every rank (the RCCL id)
 
-// A new rendezvous id (listener opened in this process) advertising `addr`
-// (dotted IPv4; NULL = ST_COMM_ADDR / the interface choice); 0 or -1.
-int rdv_make_id(char* out, const char* addr = nullptr);
+// A new rendezvous id (listener opened in this process, bound to the address
+// it advertises: `addr`, dotted IPv4; NULL = ST_COMM_ADDR / the interface
+// choice); 0 or -1.  A listener not joined within `ttl` seconds is closed by
+// a later call.
+int rdv_make_id(char* out, const char* addr, double ttl);
+
+// Close the listener of an id this process made and has not joined: 0, or
+// 1 if there is none (joined, released, or not made here); -1 on a foreign id.
+int rdv_release(const char* id);
 
 // Join the rendezvous of `id` as `rank` of `nranks`.  The first call in the
 // process that made the id hosts it: once every rank is present it calls

@@ -8,19 +8,28 @@
 // VERDICT r04 #3).  So a missing peer must be found before RCCL is entered.
 //
 // How: st_comm_unique_id no longer hands out an RCCL id.  It opens a TCP
-// listener and returns a 128-byte rendezvous id (magic, nonce, IPv4 address
-// and port, host name).  st_comm_init on every rank joins it:
+// listener on the address it advertises and returns a 128-byte rendezvous id
+// (magic, nonce, IPv4 address and port, host name).  st_comm_init on every
+// rank joins it:
 //   * the process that made the id (the first of its st_comm_init calls to
-//     claim the listener) is the host: it accepts one hello per other rank
-//     (nonce, nranks, rank, device, pid, host) until all nranks are present
-//     or the deadline (st_set_comm_timeout) passes;
+//     claim the listener) is the host.  It keeps one poll set over the
+//     listener and every connection not yet identified, so a stray or slow
+//     connector costs nobody else time: each has 5 s to present a hello
+//     (nonce, nranks, rank, device, pid, host) or is dropped.  Identified
+//     ranks are watched too: one that hangs up (it gave up at its own
+//     deadline) counts as absent again;
 //   * every other rank connects (retrying while the host is not listening
-//     yet), sends its hello and waits for the host's reply;
-//   * all present: the host makes the RCCL unique id (ncclGetUniqueId) and
-//     sends it in the reply; every rank then enters ncclCommInitRankConfig
-//     knowing that every peer is alive and about to do the same;
+//     yet), sends its hello and waits for the host's replies;
+//   * all present and alive: the host makes the RCCL unique id
+//     (ncclGetUniqueId) and sends it (phase 1); every rank acknowledges it;
+//     only with every acknowledgement in does the host send "go" (phase 2),
+//     and only on "go" does any rank enter ncclCommInitRankConfig.  A rank
+//     that does not acknowledge makes the host send "abort" to all: all
+//     ranks enter RCCL or none does;
 //   * otherwise the host's reply names the ranks that did not arrive, every
 //     present rank returns -1 with that message, and no RCCL state exists.
+// A listener whose id is never joined is closed by st_comm_id_release, or
+// by the next st_comm_unique_id once two deadlines have passed.
 // The loop being sharded is similarity_transform.cpp:39-53; its per-round
 // host sync (:45-50) is what the all-gather over this communicator replaces.
 
@@ -53,7 +62,7 @@
 namespace st {
 namespace {
 
-constexpr char kMagic[8] = { 's', 't', '-', 'r', 'd', 'v', '1', 0 };
+constexpr char kMagic[8] = { 's', 't', '-', 'r', 'd', 'v', '2', 0 };
 
 struct RdvId // the bytes of st_comm_unique_id's id (kRdvIdBytes)
 {
@@ -76,18 +85,34 @@ struct Hello
 struct Reply
 {
   uint64_t nonce;
-  int32_t status; // 0: payload valid; else msg says why
-  int32_t reserved;
+  int32_t status; // 0: payload valid (phase 1) / go (phase 2); else msg says why
+  int32_t phase;  // 1: the RCCL id, 2: go / abort
   char payload[kRdvPayloadBytes];
   char msg[512];
 };
 
-// listeners made by st_comm_unique_id in this process, by nonce; the first
-// st_comm_init that joins an id found here is its host
-std::mutex g_mu;
-std::unordered_map<uint64_t, int> g_listeners;
+struct Ack // a peer's receipt of the phase-1 id
+{
+  uint64_t nonce;
+  int32_t rank, ok;
+};
+
+// how long an accepted connection may take to present its hello, and the
+// host waits for the acknowledgements (peers answer at once)
+constexpr double kHelloS = 5.0;
+constexpr double kAckS = 10.0;
 
 using Clock = std::chrono::steady_clock;
+
+// listeners made by st_comm_unique_id in this process, by nonce; the first
+// st_comm_init that joins an id found here is its host
+struct Listener
+{
+  int fd;
+  Clock::time_point expires; // reaped by a later st_comm_unique_id after this
+};
+std::mutex g_mu;
+std::unordered_map<uint64_t, Listener> g_listeners;
 
 double
 seconds_since(Clock::time_point t0)
@@ -229,13 +254,14 @@ rank_list(const std::vector<int>& r)
 }
 
 int
-reply_all(const std::vector<int>& fds, uint64_t nonce, int status,
+reply_all(const std::vector<int>& fds, uint64_t nonce, int phase, int status,
           const char* payload, const std::string& msg)
 {
   Reply rp;
   std::memset(&rp, 0, sizeof rp);
   rp.nonce = nonce;
   rp.status = status;
+  rp.phase = phase;
   if (payload)
     std::memcpy(rp.payload, payload, kRdvPayloadBytes);
   std::snprintf(rp.msg, sizeof rp.msg, "%s", msg.c_str());
@@ -256,58 +282,165 @@ close_all(std::vector<int>& fds)
     }
 }
 
-// the host side: collect a hello from every other rank, then reply
+// an identified rank's connection: false once the peer has hung up (EOF
+// pending, or an error) - it gave up at its own deadline
+bool
+peer_alive(int fd)
+{
+  pollfd p{ fd, (short)(POLLIN | POLLRDHUP), 0 };
+  if (poll(&p, 1, 0) <= 0)
+    return true; // nothing pending: still connected
+  if (p.revents & (POLLERR | POLLHUP | POLLRDHUP | POLLNVAL))
+    return false;
+  char c;
+  const ssize_t r = recv(fd, &c, 1, MSG_PEEK | MSG_DONTWAIT);
+  return r > 0 || (r < 0 && (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR));
+}
+
+Clock::time_point
+after(Clock::time_point t, double s)
+{
+  return t + std::chrono::duration_cast<Clock::duration>(std::chrono::duration<double>(s));
+}
+
+int
+ms_left(Clock::time_point until)
+{
+  const auto l =
+    std::chrono::ceil<std::chrono::milliseconds>(until - Clock::now()).count();
+  return l <= 0 ? 0 : (int)std::min<long long>(l, 200);
+}
+
+// a connection accepted but not yet identified
+struct Pending
+{
+  int fd;
+  Clock::time_point until; // its hello's deadline
+  size_t got;              // bytes of the hello read so far
+  Hello h;
+};
+
+// the host side: collect a hello from every other rank, hand out the id,
+// collect the acknowledgements, then go (or abort)
 int
 host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
           const std::function<int(char*)>& make_payload, char* payload)
 {
   const auto t0 = Clock::now();
-  const auto until = t0 + std::chrono::duration_cast<Clock::duration>(
-                            std::chrono::duration<double>(limit));
+  const auto until = after(t0, limit);
   std::vector<int> fds(nranks, -1); // fds[r]: rank r's connection
+  std::vector<int> gone;            // ranks that hung up after their hello
+  std::vector<Pending> pend;
   int present = 1;
   std::string fail;
+  auto refuse = [&](int c, const Hello& h) {
+    char b[400];
+    const bool dup = (h.rank >= 0 && h.rank < nranks && fds[h.rank] >= 0) || h.rank == rank;
+    std::snprintf(b, sizeof b,
+                  "rank %d (pid %d on %s) joined with nranks %d; the id's host is "
+                  "rank %d of %d%s",
+                  h.rank, h.pid, h.host, h.nranks, rank, nranks,
+                  dup ? " and that rank is already present" : "");
+    fail = b;
+    std::vector<int> one_fd{ c };
+    reply_all(one_fd, id.nonce, 1, 2, nullptr, fail);
+  };
   while (present < nranks && fail.empty()) {
-    const auto left =
-      std::chrono::ceil<std::chrono::milliseconds>(until - Clock::now())
-        .count();
-    if (left <= 0)
+    const int wait = ms_left(until);
+    if (wait <= 0 && Clock::now() >= until)
       break;
-    if (!wait_fd(lfd, POLLIN, (int)std::min<long long>(left, 200)))
-      continue;
-    const int c = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC); // blocking
-    if (c < 0)
-      continue; // EAGAIN (reset in between) or EINTR: poll again
-    int one = 1;
-    setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
-    Hello h;
-    // a hello follows the connect at once; 5 s covers a loaded host
-    const auto h_until = std::min(until, Clock::now() + std::chrono::seconds(5));
-    if (!read_all(c, &h, sizeof h, h_until) || h.nonce != id.nonce) {
-      close(c); // not one of ours (or it gave up): ignore it
-      continue;
-    }
-    h.host[sizeof h.host - 1] = 0;
-    if (h.nranks != nranks || h.rank < 0 || h.rank >= nranks || h.rank == rank ||
-        fds[h.rank] >= 0) {
-      char b[400];
-      std::snprintf(b, sizeof b,
-                    "rank %d (pid %d on %s) joined with nranks %d; the id's "
-                    "host is rank %d of %d%s",
-                    h.rank, h.pid, h.host, h.nranks, rank, nranks,
-                    (h.rank >= 0 && h.rank < nranks && fds[h.rank] >= 0) ||
-                        h.rank == rank
-                      ? " and that rank is already present"
-                      : "");
-      fail = b;
-      std::vector<int> one_fd{ c };
-      reply_all(one_fd, id.nonce, 2, nullptr, fail);
-      close(c);
+    // one poll over the listener, the unidentified connections and the
+    // identified ranks (hang-ups)
+    std::vector<pollfd> ps;
+    ps.push_back({ lfd, POLLIN, 0 });
+    for (const Pending& q : pend)
+      ps.push_back({ q.fd, POLLIN, 0 });
+    std::vector<int> watched;
+    for (int r = 0; r < nranks; r++)
+      if (fds[r] >= 0) {
+        ps.push_back({ fds[r], (short)(POLLIN | POLLRDHUP), 0 });
+        watched.push_back(r);
+      }
+    int pr = poll(ps.data(), ps.size(), wait);
+    if (pr < 0 && errno != EINTR)
       break;
+    const auto now = Clock::now();
+    // hung-up ranks first (their slot may be taken again)
+    for (size_t i = 0; i < watched.size(); i++) {
+      const pollfd& q = ps[1 + pend.size() + i];
+      if (q.revents && !peer_alive(q.fd)) {
+        const int r = watched[i];
+        close(fds[r]);
+        fds[r] = -1;
+        present--;
+        gone.push_back(r);
+      }
     }
-    fds[h.rank] = c;
-    present++;
+    // hellos: read what is there, never block
+    std::vector<Pending> keep;
+    for (size_t i = 0; i < pend.size(); i++) {
+      Pending q = pend[i];
+      bool drop = now >= q.until; // too slow: not one of ours
+      if (!drop && (ps[1 + i].revents & (POLLIN | POLLHUP | POLLERR))) {
+        const ssize_t r = recv(q.fd, reinterpret_cast<char*>(&q.h) + q.got,
+                               sizeof q.h - q.got, MSG_DONTWAIT);
+        if (r == 0 || (r < 0 && errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR))
+          drop = true;
+        else if (r > 0)
+          q.got += (size_t)r;
+      }
+      if (!drop && q.got == sizeof q.h) {
+        Hello& h = q.h;
+        h.host[sizeof h.host - 1] = 0;
+        if (h.nonce != id.nonce) {
+          drop = true; // someone else's connection
+        } else if (h.nranks != nranks || h.rank < 0 || h.rank >= nranks || h.rank == rank ||
+                   fds[h.rank] >= 0) {
+          refuse(q.fd, h);
+          drop = true;
+        } else {
+          fds[h.rank] = q.fd;
+          present++;
+          gone.erase(std::remove(gone.begin(), gone.end(), h.rank), gone.end());
+          continue;
+        }
+      }
+      if (drop)
+        close(q.fd);
+      else
+        keep.push_back(q);
+    }
+    pend.swap(keep);
+    if (!fail.empty())
+      break;
+    // new connections (the listener is non-blocking)
+    if (ps[0].revents & POLLIN)
+      for (;;) {
+        const int c = accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC | SOCK_NONBLOCK);
+        if (c < 0)
+          break; // EAGAIN: none left (or reset in between)
+        int one = 1;
+        setsockopt(c, IPPROTO_TCP, TCP_NODELAY, &one, sizeof one);
+        Pending q;
+        q.fd = c;
+        q.until = std::min(until, after(Clock::now(), kHelloS));
+        q.got = 0;
+        std::memset(&q.h, 0, sizeof q.h);
+        pend.push_back(q);
+      }
   }
+  for (Pending& q : pend)
+    close(q.fd);
+  // everyone identified: are they all still there (a stale hello from a peer
+  // that gave up sits in the backlog until accepted)?
+  if (fail.empty() && present == nranks)
+    for (int r = 0; r < nranks; r++)
+      if (fds[r] >= 0 && !peer_alive(fds[r])) {
+        close(fds[r]);
+        fds[r] = -1;
+        present--;
+        gone.push_back(r);
+      }
   if (fail.empty() && present < nranks) {
     std::vector<int> missing, here{ rank };
     for (int r = 0; r < nranks; r++)
@@ -318,43 +451,80 @@ host_join(int lfd, const RdvId& id, int nranks, int rank, double limit,
           here.push_back(r);
       }
     std::sort(here.begin(), here.end());
+    std::sort(gone.begin(), gone.end());
     char b[480];
     std::snprintf(b, sizeof b,
                   "RCCL rank%s %s of %d did not reach st_comm_init within %.1f s "
-                  "(ST_COMM_TIMEOUT_S / st_set_comm_timeout; present: %s; the "
+                  "(ST_COMM_TIMEOUT_S / st_set_comm_timeout; present: %s%s%s; the "
                   "id's host is rank %d on %s): no rank entered RCCL",
                   missing.size() > 1 ? "s" : "", rank_list(missing).c_str(), nranks,
-                  seconds_since(t0), rank_list(here).c_str(), rank, id.host);
+                  seconds_since(t0), rank_list(here).c_str(),
+                  gone.empty() ? "" : "; hung up after arriving: ",
+                  rank_list(gone).c_str(), rank, id.host);
     fail = b;
   }
   if (fail.empty() && make_payload(payload) != 0)
     fail = std::string("the id's host (rank ") + std::to_string(rank) +
            ") could not make the RCCL id";
-  if (fail.empty()) {
-    const int bad = reply_all(fds, id.nonce, 0, payload, "");
+  if (!fail.empty()) {
+    reply_all(fds, id.nonce, 1, 1, nullptr, fail);
     close_all(fds);
-    if (bad) {
-      ::st::set_error("st_comm_init: %d rank(s) closed the rendezvous before "
-                      "receiving the RCCL id",
-                      bad);
-      return -1;
-    }
-    return 0;
+    ::st::set_error("st_comm_init: %s", fail.c_str());
+    return -1;
   }
-  reply_all(fds, id.nonce, 1, nullptr, fail);
+  // phase 1: the id to every rank; then every rank's acknowledgement
+  int bad = reply_all(fds, id.nonce, 1, 0, payload, "");
+  std::vector<int> silent;
+  if (bad == 0) {
+    const auto a_until = after(Clock::now(), kAckS);
+    for (int r = 0; r < nranks; r++) {
+      if (fds[r] < 0)
+        continue;
+      Ack a;
+      if (!read_all(fds[r], &a, sizeof a, a_until) || a.nonce != id.nonce || a.rank != r ||
+          a.ok != 1)
+        silent.push_back(r);
+    }
+  }
+  if (bad || !silent.empty()) {
+    char b[400];
+    if (bad)
+      std::snprintf(b, sizeof b,
+                    "%d rank(s) closed the rendezvous before receiving the RCCL id "
+                    "(the id's host is rank %d on %s): no rank entered RCCL",
+                    bad, rank, id.host);
+    else
+      std::snprintf(b, sizeof b,
+                    "RCCL rank%s %s of %d did not acknowledge the RCCL id within %.0f s "
+                    "(the id's host is rank %d on %s): no rank entered RCCL",
+                    silent.size() > 1 ? "s" : "", rank_list(silent).c_str(), nranks,
+                    kAckS, rank, id.host);
+    reply_all(fds, id.nonce, 2, 1, nullptr, b); // phase 2: abort
+    close_all(fds);
+    ::st::set_error("st_comm_init: %s", b);
+    return -1;
+  }
+  // phase 2: go
+  bad = reply_all(fds, id.nonce, 2, 0, nullptr, "");
   close_all(fds);
-  ::st::set_error("st_comm_init: %s", fail.c_str());
-  return -1;
+  if (bad) {
+    // a peer vanished between its acknowledgement and the go: the others
+    // are entering RCCL now and will meet the init deadline
+    ::st::set_error("st_comm_init: %d rank(s) closed the rendezvous after "
+                    "acknowledging the RCCL id",
+                    bad);
+    return -1;
+  }
+  return 0;
 }
 
-// any other rank: connect, hello, wait for the host's reply
+// any other rank: connect, hello, wait for the id, acknowledge, wait for go
 int
 peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
           char* payload)
 {
   const auto t0 = Clock::now();
-  const auto until = t0 + std::chrono::duration_cast<Clock::duration>(
-                            std::chrono::duration<double>(limit));
+  const auto until = after(t0, limit);
   const std::string where = ip_str(id.addr) + ":" + std::to_string(ntohs(id.port)) +
                             " (" + id.host + ")";
   int fd = -1;
@@ -411,12 +581,10 @@ peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
   // the host answers when every rank is present or at ITS deadline, which
   // may lie up to one deadline after this rank's: wait for the reply (and
   // the names it carries) that much longer
-  const auto r_until = until + std::chrono::duration_cast<Clock::duration>(
-                                 std::chrono::duration<double>(limit));
   Reply rp;
-  const bool got = read_all(fd, &rp, sizeof rp, r_until);
-  close(fd);
-  if (!got || rp.nonce != id.nonce) {
+  const bool got = read_all(fd, &rp, sizeof rp, after(until, limit));
+  if (!got || rp.nonce != id.nonce || rp.phase != 1) {
+    close(fd);
     ::st::set_error("st_comm_init: RCCL rank %d of %d: no word from the id's host "
                     "at %s after %.1f s (it failed, exited or never joined); no "
                     "rank entered RCCL",
@@ -425,25 +593,63 @@ peer_join(const RdvId& id, int nranks, int rank, int device, double limit,
   }
   rp.msg[sizeof rp.msg - 1] = 0;
   if (rp.status != 0) {
+    close(fd);
     ::st::set_error("st_comm_init: %s", rp.msg);
     return -1;
   }
   std::memcpy(payload, rp.payload, kRdvPayloadBytes);
+  Ack a{ id.nonce, rank, 1 };
+  Reply go;
+  const bool acked = write_all(fd, &a, sizeof a);
+  // the host decides within its acknowledgement window
+  const bool heard = acked && read_all(fd, &go, sizeof go, after(Clock::now(), kAckS + 5.0));
+  close(fd);
+  if (!heard || go.nonce != id.nonce || go.phase != 2) {
+    ::st::set_error("st_comm_init: RCCL rank %d of %d: the id's host at %s did not "
+                    "confirm the RCCL id after %.1f s; no rank entered RCCL",
+                    rank, nranks, where.c_str(), seconds_since(t0));
+    return -1;
+  }
+  go.msg[sizeof go.msg - 1] = 0;
+  if (go.status != 0) {
+    ::st::set_error("st_comm_init: %s", go.msg);
+    return -1;
+  }
   return 0;
 }
 
 } // namespace
 
 int
-rdv_make_id(char* out, const char* addr)
+rdv_make_id(char* out, const char* addr, double ttl)
 {
+  if (addr) {
+    in_addr a;
+    ST_REQUIRE(inet_pton(AF_INET, addr, &a) == 1,
+               "st_comm_unique_id_addr: %s is not an IPv4 address", addr);
+  }
+  // listeners of ids never joined, past two deadlines: nobody will come
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    const auto now = Clock::now();
+    for (auto it = g_listeners.begin(); it != g_listeners.end();)
+      if (it->second.expires <= now) {
+        close(it->second.fd);
+        it = g_listeners.erase(it);
+      } else {
+        ++it;
+      }
+  }
   // non-blocking: accept after poll must not block on a connection that
   // was reset in between (host_join polls, then accepts)
   const int fd = socket(AF_INET, SOCK_STREAM | SOCK_CLOEXEC | SOCK_NONBLOCK, 0);
   ST_REQUIRE(fd >= 0, "st_comm_unique_id: socket: %s", std::strerror(errno));
+  // listen on the address the id advertises only (loopback for a one-host
+  // group), not on every interface
+  const uint32_t adv = advertised_addr(addr);
   sockaddr_in sa{};
   sa.sin_family = AF_INET;
-  sa.sin_addr.s_addr = htonl(INADDR_ANY);
+  sa.sin_addr.s_addr = adv;
   sa.sin_port = 0;
   socklen_t sl = sizeof sa;
   if (bind(fd, reinterpret_cast<sockaddr*>(&sa), sizeof sa) != 0 ||
@@ -451,7 +657,8 @@ rdv_make_id(char* out, const char* addr)
       getsockname(fd, reinterpret_cast<sockaddr*>(&sa), &sl) != 0) {
     const int e = errno;
     close(fd);
-    ::st::set_error("st_comm_unique_id: listener: %s", std::strerror(e));
+    ::st::set_error("st_comm_unique_id: listener on %s: %s", ip_str(adv).c_str(),
+                    std::strerror(e));
     return -1;
   }
   RdvId id;
@@ -464,23 +671,31 @@ rdv_make_id(char* out, const char* addr)
     id.nonce ^= ((uint64_t)rd() << 32) ^ rd();
   } catch (...) { // no entropy source: pid, time and fd still differ per id
   }
-  if (addr) {
-    in_addr a;
-    if (inet_pton(AF_INET, addr, &a) != 1) {
-      close(fd);
-      ::st::set_error("st_comm_unique_id_addr: %s is not an IPv4 address", addr);
-      return -1;
-    }
-  }
-  id.addr = advertised_addr(addr);
+  id.addr = adv;
   id.port = sa.sin_port;
   host_name(id.host, sizeof id.host);
   {
     std::lock_guard<std::mutex> lk(g_mu);
-    g_listeners[id.nonce] = fd;
+    g_listeners[id.nonce] = Listener{ fd, after(Clock::now(), ttl) };
   }
   std::memset(out, 0, kRdvIdBytes);
   std::memcpy(out, &id, sizeof id);
+  return 0;
+}
+
+int
+rdv_release(const char* id_in)
+{
+  RdvId id;
+  std::memcpy(&id, id_in, sizeof id);
+  ST_REQUIRE(std::memcmp(id.magic, kMagic, sizeof kMagic) == 0,
+             "st_comm_id_release: the id was not made by st_comm_unique_id");
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_listeners.find(id.nonce);
+  if (it == g_listeners.end())
+    return 1; // not this process's, or already joined / released
+  close(it->second.fd);
+  g_listeners.erase(it);
   return 0;
 }
 
@@ -498,7 +713,7 @@ rdv_join(const char* id_in, int nranks, int rank, int device, double limit,
     std::lock_guard<std::mutex> lk(g_mu);
     auto it = g_listeners.find(id.nonce);
     if (it != g_listeners.end()) {
-      lfd = it->second;
+      lfd = it->second.fd;
       g_listeners.erase(it);
     }
   }

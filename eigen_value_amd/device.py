@@ -217,10 +217,16 @@ def flat_round(mat, s_cur, s_next, part, v, state, *, row0: int = 0, eps: float 
 
 
 def set_flat_grid_limit(max_x: int = 0) -> int:
-    """Testing hook (st_set_flat_grid_limit): the width past which the flat
-    launches go 2-D (0 = the default, the dispatch limit).  Returns the
-    limit in force."""
-    return int(_lib.load().st_set_flat_grid_limit(max_x))
+    """Testing hook (st_set_flat_grid_limit, include/st_tuning.h): the width
+    past which the flat launches go 2-D (0 = the default, the dispatch
+    limit).  Returns the limit in force.  The tuning build only: the
+    package's library must be libsimilarity_transform_tuning.so
+    (EIGEN_VALUE_LIB), whose launches the limit then moves."""
+    L = _lib.load()
+    if not hasattr(L, "st_set_flat_grid_limit"):
+        raise _lib.EigenValueError("st_set_flat_grid_limit: the tuning build only "
+                                   "(EIGEN_VALUE_LIB=" + _lib.TUNING_LIB + ")")
+    return int(L.st_set_flat_grid_limit(max_x))
 
 
 def defer_rounds(nrows: int, ncols: int, dtype) -> int:

@@ -124,6 +124,30 @@ class HipShardOps:
             self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
                                  max_itr=max_itr, semantics=semantics, state=state)
 
+    def round_call(self, mat, s_cur, s_next, v, v_next, row0, eps, max_itr, semantics,
+                   state, matrix_free=False):
+        """The launch of round() (or mfree_round()) for these buffers with
+        every argument resolved but the round index: (fn, pre, post) such
+        that fn(*pre, k, *post) enqueues round k on the current stream and
+        returns the C-ABI status.  The same entry point and arguments round()
+        passes, without its per-call Python work (the bench's timed loop)."""
+        L = self.dev._lib.load()
+        sfx = self.dev._sfx(mat)
+        nrows, ncols = mat.shape
+        ptr = self.dev._ptr
+        stream = self.dev._stream(mat.device)
+        post = (max_itr, semantics, ptr(state), stream)
+        if matrix_free:
+            return (getattr(L, f"st_mfree_round_{sfx}"),
+                    (ptr(mat), ptr(s_cur), ptr(s_next), ptr(v), ptr(v_next), nrows, ncols,
+                     row0, eps), post)
+        if self.dev.flat_round_pays(nrows, ncols, mat.dtype):
+            return (getattr(L, f"st_round_flat_{sfx}"),
+                    (ptr(mat), ptr(s_cur), ptr(s_next), ptr(self._scratch(nrows, ncols, mat.dtype)),
+                     ptr(v), nrows, ncols, row0, eps), post)
+        return (getattr(L, f"st_round_{sfx}"),
+                (ptr(mat), ptr(s_cur), ptr(s_next), ptr(v), nrows, ncols, row0, eps), post)
+
     def split_round(self, mat, s_cur, s_next, part, v, row0, col0, col1, eps, k, max_itr,
                     semantics, state, span):
         # blocks where the flat round pays split it the same way
@@ -176,7 +200,8 @@ class HipShardOps:
 
 
 class PeerMissingError(_lib.EigenValueError):
-    """A rank did not reach the communicator rendezvous within the deadline.
+    """A rank did not reach the communicator rendezvous within the deadline
+    (the id hand-over, share_id, or st_comm_init's own rendezvous).
     Raised on every rank that did; ``missing`` lists the absent group ranks.
     No RCCL state exists at that point, and no collective may be issued on
     the group (it would wait for the absent rank)."""
@@ -186,7 +211,7 @@ class PeerMissingError(_lib.EigenValueError):
         self.missing = list(missing)
 
 
-_RDV_SEQ: dict = {}    # (tag, group's global ranks) -> rendezvous calls made on it
+_ID_SEQ: dict = {}    # (tag, group's global ranks) -> communicator ids handed over on it
 
 
 def _group_store(group):
@@ -202,23 +227,16 @@ def _group_store(group):
     return store
 
 
-def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=None,
-               tag: str = "comm") -> Optional[bytes]:
-    """Every rank of `group` proves presence over the group's c10d store
-    (TCP, no collective) before any rank enters RCCL: each sets its key,
-    then waits at most `timeout` seconds (default: the library's RCCL
-    deadline, st_get_comm_timeout) for every other rank's.  A rank that
-    does not arrive makes every present rank raise PeerMissingError naming
-    it - instead of the first RCCL call (init, or torch's broadcast of the
-    id) waiting for it indefinitely.
-
-    payload_from_first: called on group rank 0 once everyone is present,
-    with the ranks' host names (each rank's key holds its own); its bytes
-    (or an exception's text) reach every rank, which returns them.
-    Calls are matched across ranks by order within a group: every rank of
-    a group must make the same sequence of rendezvous calls on it."""
+def share_id(group, make, timeout: Optional[float] = None, tag: str = "comm") -> bytes:
+    """Group rank 0 calls make() and hands its bytes to every rank over the
+    group's c10d store (TCP, no collective); the others wait at most
+    `timeout` seconds (default: the library's RCCL deadline) and raise
+    PeerMissingError naming rank 0 if it never hands one over.  That is the
+    only wait here: whether every OTHER rank is present is checked by
+    st_comm_init's own rendezvous (st_rendezvous.hip), before any rank
+    enters RCCL.  make()'s exception reaches every rank as an error.  Calls
+    are matched across ranks by order within a group."""
     import datetime
-    import socket
 
     import torch.distributed as dist
     if timeout is None:
@@ -226,60 +244,54 @@ def rendezvous(group=None, timeout: Optional[float] = None, payload_from_first=N
     world, rank = dist.get_world_size(group), dist.get_rank(group)
     gkey = (tag, tuple(dist.get_global_rank(group, r) for r in range(world))
             if group is not None else None)
-    _RDV_SEQ[gkey] = seq = _RDV_SEQ.get(gkey, 0) + 1     # matched per group, by order
-    base = f"eigen_value_amd/rdv/{tag}/{seq}"
+    _ID_SEQ[gkey] = seq = _ID_SEQ.get(gkey, 0) + 1
+    key = f"eigen_value_amd/id/{tag}/{seq}"
     store = _group_store(group)
-    store.set(f"{base}/here/{rank}", socket.gethostname().encode() or b"?")
-    keys = [f"{base}/here/{r}" for r in range(world)]
-    try:
-        store.wait(keys, datetime.timedelta(seconds=timeout))
-    except Exception as e:  # noqa: BLE001 - c10d raises DistStoreError/RuntimeError
-        missing = [r for r in range(world) if not store.check([keys[r]])]
-        if not missing:       # everyone arrived as the wait gave up
-            missing = None
-        if missing is not None:
-            raise PeerMissingError(
-                f"group rank{'s' if len(missing) > 1 else ''} "
-                f"{', '.join(map(str, missing))} of {world} did not reach the communicator "
-                f"rendezvous within {timeout:.1f} s (st_set_comm_timeout / "
-                f"ST_COMM_TIMEOUT_S); this is rank {rank}; no rank entered RCCL",
-                missing) from e
-    if payload_from_first is None:
-        return None
-    key = f"{base}/payload"
     if rank == 0:
         try:
-            hosts = [store.get(k).decode(errors="replace") for k in keys]
-            data = b"ok:" + bytes(payload_from_first(hosts))
+            data = b"ok:" + bytes(make())
         except Exception as e:  # noqa: BLE001 - reaches every rank below
             data = b"error:" + f"{type(e).__name__}: {e}".encode()
         store.set(key, data)
     else:
         try:
             store.wait([key], datetime.timedelta(seconds=timeout))
-        except Exception as e:  # noqa: BLE001 - rank 0 stopped after arriving
+        except Exception as e:  # noqa: BLE001 - c10d raises DistStoreError/RuntimeError
             raise PeerMissingError(
-                f"group rank 0 of {world} arrived but did not hand over the communicator id "
-                f"within {timeout:.1f} s; this is rank {rank}; no rank entered RCCL",
-                [0]) from e
+                f"group rank 0 of {world} did not hand over the communicator id within "
+                f"{timeout:.1f} s (st_set_comm_timeout / ST_COMM_TIMEOUT_S); this is rank "
+                f"{rank}; no rank entered RCCL", [0]) from e
         data = store.get(key)
     if data.startswith(b"error:"):
         raise _lib.EigenValueError(f"group rank 0 failed: {data[6:].decode(errors='replace')}")
     return data[3:]
 
 
+def _one_host() -> bool:
+    """Every rank runs on this host: the rendezvous point is the loopback
+    address (torch.distributed.run --nnodes=1 sets LOCAL_WORLD_SIZE =
+    WORLD_SIZE; a loopback MASTER_ADDR can only be reached from here)."""
+    import os
+    if os.environ.get("MASTER_ADDR", "") in ("127.0.0.1", "localhost", "::1"):
+        return True
+    lws, ws = os.environ.get("LOCAL_WORLD_SIZE"), os.environ.get("WORLD_SIZE")
+    return lws is not None and lws == ws
+
+
 class RcclComm:
     """An RCCL communicator owned by libsimilarity_transform.so for the
-    per-round all-gather: every rank proves presence over the group's c10d
-    store (rendezvous), group rank 0 then makes the library's id and hands
-    it over the store, and every rank joins with st_comm_init (which checks
-    presence once more before RCCL is entered, st_rendezvous.hip); the
-    collective is then issued straight on the launch stream (no per-round
-    hand-off between torch's compute and communication streams)."""
+    per-round all-gather: group rank 0 makes the library's rendezvous id
+    and hands it over the group's c10d store (share_id), and every rank
+    joins with st_comm_init, whose rendezvous checks that every rank is
+    present - naming those that are not - before any rank enters RCCL
+    (st_rendezvous.hip); the collective is then issued straight on the
+    launch stream (no per-round hand-off between torch's compute and
+    communication streams)."""
 
     def __init__(self, group=None, device_index: Optional[int] = None,
                  timeout: Optional[float] = None):
         import ctypes
+        import os
 
         import torch
         import torch.distributed as dist
@@ -289,20 +301,24 @@ class RcclComm:
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         dev = torch.cuda.current_device() if device_index is None else device_index
+        made = []
 
-        def make_id(hosts):
-            # every rank on this host: the library's rendezvous advertises
-            # the loopback address (no interface choice involved), unless
-            # the caller chose one (ST_COMM_ADDR)
-            import os
-            import socket
-            local = all(h == socket.gethostname() for h in hosts)
-            addr = b"127.0.0.1" if local and "ST_COMM_ADDR" not in os.environ else None
+        def make_id():
+            # every rank on this host: the rendezvous listens on the loopback
+            # address (no interface choice involved), unless the caller
+            # chose one (ST_COMM_ADDR)
+            addr = b"127.0.0.1" if _one_host() and "ST_COMM_ADDR" not in os.environ else None
             uid = ctypes.create_string_buffer(128)
             _lib.check(self.L.st_comm_unique_id_addr(uid, addr), "st_comm_unique_id_addr")
+            made.append(uid.raw)
             return uid.raw
 
-        uid = rendezvous(group, timeout, payload_from_first=make_id)
+        try:
+            uid = share_id(group, make_id, timeout)
+        except BaseException:
+            for u in made:           # made here, never to be joined: close its listener
+                self.L.st_comm_id_release(u)
+            raise
         _lib.check(self.L.st_comm_init(ctypes.byref(self.comm), world, rank, uid, dev),
                    "st_comm_init")
         self.rank, self.world = rank, world
@@ -318,10 +334,15 @@ class RcclComm:
                 **_lib.rccl_info(self.L)}
 
     def allgather(self, out, inp) -> None:
+        fn, args = self.allgather_call(out, inp)
+        _lib.check(fn(*args), "st_allgather")
+
+    def allgather_call(self, out, inp):
+        """(fn, args): fn(*args) is allgather(out, inp) on the current stream."""
         sfx = "f64" if out.dtype == self.torch.float64 else "f32"
         stream = self.torch.cuda.current_stream(out.device).cuda_stream
-        _lib.check(getattr(self.L, f"st_allgather_{sfx}")(
-            self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), stream), "st_allgather")
+        return (getattr(self.L, f"st_allgather_{sfx}"),
+                (self.comm, inp.data_ptr(), out.data_ptr(), inp.numel(), stream))
 
     def close(self) -> None:
         if self.comm is not None and self.comm.value:
@@ -545,6 +566,53 @@ class ShardedSimilarityTransform:
         self.gather(self.s[cur ^ 1])
         self.cur = cur ^ 1
         self.k += 1
+
+    def rounds(self, count: int, eps: float, max_itr: int) -> None:
+        """``count`` calls of round(), enqueued through pre-resolved launches
+        (HipShardOps.round_call; the library all-gather's likewise): the same
+        kernels, arguments and exchange, without round()'s per-call Python
+        work between launches.  Falls back to round() where the ops or the
+        schedule (overlap, torch's all-gather) have no such path."""
+        p = self.part
+        gather_ok = p.world == 1 or self.rehearsal or self.rccl is not None
+        if self.overlap or not gather_ok or not hasattr(self.ops, "round_call") \
+                or (self.cur != (self.k & 1)):
+            for _ in range(count):
+                self.round(eps, max_itr)
+            return
+        key = (eps, max_itr, self.mat.data_ptr(), self.torch.cuda.current_stream().cuda_stream)
+        if getattr(self, "_calls_key", None) != key:
+            calls = []
+            for par in (0, 1):
+                if self.matrix_free:
+                    c = self.ops.round_call(self.mat, self.s[par][:p.n], self._slot(self.s[par ^ 1]),
+                                            self.vb[par][:p.n], self.vb[par ^ 1][:p.n], p.row0,
+                                            eps, max_itr, self.semantics, self.state,
+                                            matrix_free=True)
+                else:
+                    c = self.ops.round_call(self.mat, self.s[par][:p.n], self._slot(self.s[par ^ 1]),
+                                            self.v, None, p.row0, eps, max_itr, self.semantics,
+                                            self.state)
+                g = None
+                if p.world > 1 and not self.rehearsal:
+                    g = self.rccl.allgather_call(self.s[par ^ 1],
+                                                 self.s[par ^ 1][p.rank * p.chunk:(p.rank + 1) * p.chunk])
+                calls.append((c, g))
+            self._calls, self._calls_key = calls, key
+        L = _lib.load()
+        for _ in range(count):
+            (fn, pre, post), g = self._calls[self.k & 1]
+            # the matrix-free launch k + 1 evaluates round k (round())
+            kk = self.k + 1 if self.matrix_free else self.k
+            rc = fn(*pre, kk, *post)
+            if rc < 0:
+                _lib.check(rc, "round", L)
+            if g is not None:
+                rc = g[0](*g[1])
+                if rc < 0:
+                    _lib.check(rc, "st_allgather", L)
+            self.cur ^= 1
+            self.k += 1
 
     def _round_overlap(self, eps: float, max_itr: int, events=None):
         """Round k with the all-gather of s_k overlapping the local half:

@@ -27,6 +27,12 @@
 
 #include <stdint.h>
 
+/* the library is built with -fvisibility=hidden: what this header declares
+ * is its whole dynamic ABI */
+#if defined(__GNUC__)
+#pragma GCC visibility push(default)
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -198,14 +204,17 @@ int64_t st_solve_multi_f64(const double* mat, unsigned int dim, int ngpus,
  * ncclAllGather on `stream` (in place when send = recv + rank*count).
  *
  * Presence before RCCL: the id is a rendezvous id, not an RCCL one - the
- * maker listens on a TCP port (address: ST_COMM_ADDR, else the first IPv4
- * address of NCCL_SOCKET_IFNAME's or of the first up non-loopback
- * interface, else 127.0.0.1).  st_comm_init on every rank first joins it;
- * only when all nranks are present does the maker create the RCCL id and
- * hand it to all, and only then does any rank enter ncclCommInitRankConfig.
- * A rank that does not arrive within the deadline makes st_comm_init return
- * -1 on every present rank, eigen_last_error() naming the missing ranks,
- * with no RCCL state created (the process exits normally).
+ * maker listens on a TCP port of the address it advertises (ST_COMM_ADDR,
+ * else the first IPv4 address of NCCL_SOCKET_IFNAME's or of the first up
+ * non-loopback interface, else 127.0.0.1).  st_comm_init on every rank
+ * first joins it; only when all nranks are present (and still connected)
+ * does the maker create the RCCL id and hand it to all, every rank
+ * acknowledges it, and only on the maker's final "go" does any rank enter
+ * ncclCommInitRankConfig (all ranks enter RCCL or none does).  A rank that
+ * does not arrive within the deadline makes st_comm_init return -1 on every
+ * present rank, eigen_last_error() naming the missing ranks, with no RCCL
+ * state created (the process exits normally).  Connections that present no
+ * hello within 5 s are dropped without delaying the others.
  *
  * Deadline: every communicator is non-blocking (ncclConfig_t.blocking = 0)
  * and each step that waits for peers - the rendezvous, st_comm_init's RCCL
@@ -224,6 +233,12 @@ int st_comm_unique_id(char* id_out);
 int st_comm_unique_id_addr(char* id_out, const char* addr);
 int st_comm_init(void** comm, int nranks, int rank, const char* id_in,
                  int device);
+/* Close the listener of an id this process made and will not join (e.g. its
+ * maker failed before st_comm_init): 0, or 1 if there is none (already
+ * joined or released, or made elsewhere).  An id never joined nor released
+ * is closed by a later st_comm_unique_id once 2 x the deadline + 30 s have
+ * passed. */
+int st_comm_id_release(const char* id);
 int st_comm_destroy(void* comm);
 /* Set the RCCL deadline in seconds (<= 0: back to ST_COMM_TIMEOUT_S / 120);
  * returns the previous effective value.  Process-wide. */
@@ -379,78 +394,6 @@ int st_round_flat_f64(double* d_mat, const double* d_s_cur, double* d_s_next,
                       unsigned int semantics, st_state* d_state, void* stream);
 uint64_t st_round_flat_scratch(unsigned int nrows, unsigned int ncols);
 int st_round_flat_pays(unsigned int nrows, unsigned int ncols, int dtype);
-/* Testing hook: the flat launches (k_flat, one workgroup per piece) spread
- * more workgroups than a dispatch's 2^32 - 1 work-items per dimension allow
- * (fp64 from 131072^2) over a 2-D grid of rows at most max_x wide; this lowers
- * max_x (rounded down to a multiple of 8, at least 8; 0 restores the
- * default, 16777208) so the 2-D form can be checked at small sizes.
- * Process-wide; returns the limit now in force.  Results do not depend on
- * it. */
-unsigned int st_set_flat_grid_limit(unsigned int max_x);
-
-/* Workgroups per CU of the deferred flat round's launches (dtype 0 = f32,
- * 1 = f64; nontemporal = the launch form of blocks >= 2 GiB, else the cached
- * one; slot 0..4 = a read-only round with that many pending rounds, 6 =
- * a storing round; wg_per_cu 0 = uncapped, else 2..32).  The library's
- * defaults are measured (DESIGN.md §Deferred writes); this overrides one for
- * the process, for tuning tools.  Results do not depend on it.  Returns the
- * previous value, or -1 on bad arguments. */
-int st_set_defer_caps(int dtype, int nontemporal, unsigned int slot,
-                      unsigned int wg_per_cu);
-
-/* Non-temporal matrix loads in the deferred flat round's launches on cached
- * fp64 blocks (below 2 GiB): bit NP (0..4) for a read-only round with NP
- * pending rounds, bit 6 for a storing round (bit 7: its stores non-temporal
- * as well), per block size class
- * (st_defer_ntload_class: 0 below 384 MiB, 1 below 640 MiB, 2 above).  The
- * library's defaults are measured (DESIGN.md §Deferred writes); this
- * overrides one for the process, for tuning tools.  Results do not depend
- * on it.  Returns the previous mask, or -1 on bad arguments. */
-int st_set_defer_ntload(unsigned int size_class, unsigned int mask);
-
-/* The deferred rounds' cache policy in general: for dtype (0 = f32, 1 = f64)
- * and size class (as st_set_every_cache: 0 below 384 MiB, 1 below 640 MiB,
- * 2 below 2 GiB - the cached form - and 3 from 2 GiB - the non-temporal
- * form), bit NP (0..4) of a read-only round with NP pending and bit 6 of a
- * storing round turn that launch's matrix loads over (cached <->
- * non-temporal), bit 7 the storing round's stores.  fp64 classes 0..2 are
- * st_set_defer_ntload's masks.  For tuning tools; results do not depend on
- * it.  Returns the previous mask, or -1 on bad arguments. */
-int st_set_defer_cache(int dtype, unsigned int size_class, unsigned int mask);
-
-/* The size class st_set_defer_ntload indexes for an nrows x ncols block
- * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
-int st_defer_ntload_class(unsigned int nrows, unsigned int ncols, int dtype);
-
-/* Cache policy of the every-round flat launch (the vector path): bit 0 turns
- * the matrix loads' policy over (cached <-> non-temporal), bit 1 the
- * stores', 0 = the form's own, per block size class (st_every_cache_class:
- * 0 below 384 MiB, 1 below 640 MiB, 2 below 2 GiB - the cached form - and
- * 3 from 2 GiB - the non-temporal form).  The library's defaults are
- * measured; this overrides one for the process, for
- * tuning tools.  Results do not depend on it.  Returns the previous policy,
- * or -1 on bad arguments. */
-int st_set_every_cache(unsigned int size_class, unsigned int policy);
-
-/* Workgroups per CU of the every-round flat launch per size class (the
- * classes of st_set_every_cache; 0 = uncapped, else 2..32), held by dynamic
- * LDS the kernel does not use.  For tuning tools; results do not depend on
- * it.  Returns the previous value, or -1 on bad arguments. */
-int st_set_every_caps(unsigned int size_class, unsigned int wg_per_cu);
-
-/* Piece order of the every-round flat launch per size class (the classes of
- * st_set_every_cache): 0 = the library's measured table, 1 = row-major,
- * t > 1 = tiles of t row groups per piece.  For tuning tools; results do not
- * depend on it.  Returns the previous value, or -1 on bad arguments. */
-int st_set_every_tile(unsigned int size_class, unsigned int tile);
-
-/* Launch shape of the matrix-free round (k_mfree) for every block of
- * >= 2 x 256 row groups: 0 = the library's measured table, 1 / 2 = cached
- * loads, 2 / 4 rows per group, 3 = non-temporal loads, 4 rows.  For tuning
- * tools; results do not depend on it.  Returns the previous value, or -1
- * on bad arguments. */
-int st_set_mfree_shape(unsigned int shape);
-
 /* The launch policy, as one map: what the solve loops launch for an
  * nrows x ncols block of `dtype` (0 fp32, 1 fp64; vector path, ncols a
  * multiple of 16 / sizeof element) in `form`, with `npend` pending rounds for
@@ -483,10 +426,6 @@ typedef struct st_launch_policy
 } st_launch_policy;
 int st_launch_policy_query(int dtype, unsigned int nrows, unsigned int ncols,
                            int form, unsigned int npend, st_launch_policy* out);
-
-/* The size class st_set_every_cache indexes for an nrows x ncols block
- * (dtype 0 = f32, 1 = f64), or -1 on a bad dtype. */
-int st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype);
 
 /* Round k of the flat round with deferred writes (what the solve loops run
  * for blocks where st_round_flat_pays): the matrix in d_mat is the last
@@ -656,7 +595,13 @@ int st_device_count(void);
 
 #ifdef __cplusplus
 } /* extern "C" */
+#endif
 
+#if defined(__GNUC__)
+#pragma GCC visibility pop
+#endif
+
+#ifdef __cplusplus
 /* C++ entry mirroring include/similarity_transform.hpp:46-53
  * (int64_t similarity_transform(sycl::queue&, const float* mat, float*
  * eigen_val, float* eigen_vec, uint dim, uint wg_size, uint* iter_count)).

@@ -7,18 +7,26 @@
  * step kernels' argument checks, the policy query over every form and size
  * class, the tuning setters and their range checks, the communicator calls'
  * argument errors, the deadline setter, st_comm_init's pre-RCCL rendezvous
- * - a missing rank, and three ranks as threads of this process - and the
- * RCCL version query), so the host-side parsing, error formatting
+ * - a missing rank, three ranks as threads of this process, three ranks
+ * beside a stray connector that never says hello and one that sends
+ * garbage, a rank that hung up before the host joined, an id released
+ * unjoined - and the RCCL version query), so the host-side parsing, error formatting
  * (eigen_last_error), table lookups and socket code run under the
  * sanitizers.
  * Exit 0 = clean.
  */
+#include <arpa/inet.h>
+#include <netinet/in.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <string.h>
+#include <sys/socket.h>
+#include <time.h>
+#include <unistd.h>
 
 #include "similarity_transform.h"
+#include "st_tuning.h" /* built with -DST_TUNING_ABI=1 (tools/host_asan.sh) */
 
 static int fails = 0;
 
@@ -42,6 +50,32 @@ join_rank(void* arg)
   }
   return NULL;
 }
+/* a TCP connection to the id's listener (address and port at bytes 16..21
+   of the id, network order), as a stray or hostile connector would make */
+static int
+connect_to_id(const char* idb)
+{
+  struct sockaddr_in sa;
+  memset(&sa, 0, sizeof sa);
+  sa.sin_family = AF_INET;
+  memcpy(&sa.sin_addr.s_addr, idb + 16, 4);
+  memcpy(&sa.sin_port, idb + 20, 2);
+  const int fd = socket(AF_INET, SOCK_STREAM, 0);
+  if (fd >= 0 && connect(fd, (struct sockaddr*)&sa, sizeof sa) != 0) {
+    close(fd);
+    return -1;
+  }
+  return fd;
+}
+
+static double
+now_s(void)
+{
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec + 1e-9 * ts.tv_nsec;
+}
+
 #define CHECK(c)                                                                 \
   do {                                                                           \
     if (!(c)) {                                                                  \
@@ -75,13 +109,13 @@ main(void)
                                            { 32768, 32768 }, { 8192, 65536 }, { 5824, 11648 } };
   for (int d = 0; d < 2; d++)
     for (size_t i = 0; i < sizeof sizes / sizeof sizes[0]; i++)
-      for (int form = 0; form <= 3; form++)
+      for (int form = 0; form <= 4; form++)
         for (unsigned int np = 0; np < 7; np++) {
           st_launch_policy p;
           memset(&p, 0xff, sizeof p);
           const int rc = st_launch_policy_query(d, sizes[i][0], sizes[i][1], form, np, &p);
           if (rc == 0)
-            CHECK(p.rows >= 1 && p.rows <= 8 && p.kernel >= 0 && p.kernel <= 3);
+            CHECK(p.rows >= 1 && p.rows <= 8 && p.kernel >= 0 && p.kernel <= 5);
           else
             CHECK(strlen(eigen_last_error()) > 0);
         }
@@ -131,6 +165,33 @@ main(void)
     pthread_join(th[i], NULL);
   for (int i = 0; i < 3; i++)
     CHECK(joined[i] == 0 || joined[i] == 1);
+  /* a stray connector that never says hello and one that sends garbage,
+     connected before the ranks: the host drops them without holding up the
+     three ranks (the hellos are read from one poll set) */
+  st_set_comm_timeout(20.0);
+  CHECK(st_comm_unique_id(rdv_id) == 0);
+  const int stray = connect_to_id(rdv_id), noisy = connect_to_id(rdv_id);
+  CHECK(stray >= 0 && noisy >= 0);
+  if (noisy >= 0)
+    CHECK(write(noisy, "GET / HTTP/1.0\r\n\r\n", 18) == 18);
+  for (int i = 0; i < 3; i++)
+    joined[i] = 2;
+  double t_s = now_s();
+  for (int i = 0; i < 3; i++)
+    pthread_create(&th[i], NULL, join_rank, &ranks[i]);
+  for (int i = 0; i < 3; i++)
+    pthread_join(th[i], NULL);
+  for (int i = 0; i < 3; i++)
+    CHECK(joined[i] == 0 || joined[i] == 1);
+  CHECK(now_s() - t_s < 4.0); /* not the stray's 5 s hello window */
+  if (stray >= 0)
+    close(stray);
+  if (noisy >= 0)
+    close(noisy);
+  /* the released id: its listener is closed, a peer cannot reach it */
+  CHECK(st_comm_unique_id(rdv_id) == 0);
+  CHECK(st_comm_id_release(rdv_id) == 0 && st_comm_id_release(rdv_id) == 1);
+  CHECK(connect_to_id(rdv_id) < 0);
   st_set_comm_timeout(0.0);
   int vcode = 0;
   char vpath[512];

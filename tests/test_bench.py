@@ -136,9 +136,10 @@ def test_stalled_ranks_are_ended_by_the_parent_deadline():
 
 def test_stalled_rank_is_named_by_the_communicator_rendezvous():
     """--stall-rank 1 --stall-in rendezvous: ranks 0 and 2 of a gloo world 3
-    make the library communicator's presence check (sharded.rendezvous, the
-    step before any rank enters RCCL) and name rank 1 within --comm-timeout
-    (3 s), then the run ends non-zero without a JSON line."""
+    take the library communicator as a sharded solve does; st_comm_init's
+    presence check (the step before any rank enters RCCL) names rank 1
+    within --comm-timeout (3 s), then the run ends non-zero without a JSON
+    line."""
     import time
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     t0 = time.time()
@@ -149,8 +150,9 @@ def test_stalled_rank_is_named_by_the_communicator_rendezvous():
     el = time.time() - t0
     assert out.returncode != 0, out.stderr[-3000:]
     assert not [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
-    assert "group rank 1 of 3 did not reach the communicator rendezvous within 3.0 s" \
-        in out.stderr, out.stderr[-3000:]
+    assert "RCCL rank 1 of 3 did not reach st_comm_init within 3.0 s" in out.stderr, \
+        out.stderr[-3000:]
+    assert "no rank entered RCCL" in out.stderr
     assert el < 100
 
 

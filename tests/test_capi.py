@@ -30,6 +30,34 @@ def test_exports_every_declared_symbol():
         assert getattr(L, s) is not None
 
 
+def _exported(path):
+    out = subprocess.run(["nm", "-D", "--defined-only", path],
+                         capture_output=True, text=True, check=True).stdout
+    return {line.split()[-1] for line in out.splitlines() if " T " in line}
+
+
+def test_product_library_exports_no_tuning_setter():
+    """The library drop-in callers load exports the product ABI only
+    (VERDICT r05 #5): no launch-table setter of include/st_tuning.h, no
+    st_set_* but the context's stream and the RCCL deadline."""
+    exported = _exported(_lib.lib_path())
+    tuning = _lib.declared_symbols(_lib.TUNING_HEADER)
+    assert len(tuning) == 10 and not (set(tuning) & exported), set(tuning) & exported
+    assert sorted(e for e in exported if e.startswith("st_set_")) == \
+        ["st_set_comm_timeout", "st_set_stream"]
+    assert not (exported - set(_lib.declared_symbols())), exported - set(_lib.declared_symbols())
+
+
+def test_tuning_build_exports_the_tuning_abi():
+    """libsimilarity_transform_tuning.so: the product ABI plus st_tuning.h."""
+    assert os.path.exists(_lib.TUNING_LIB), "run `make` first"
+    exported = _exported(_lib.TUNING_LIB)
+    want = set(_lib.declared_symbols()) | set(_lib.declared_symbols(_lib.TUNING_HEADER))
+    assert not (want - exported), want - exported
+    L = _lib.load_tuning()
+    assert L.st_set_flat_grid_limit(0) == 16777208
+
+
 def test_drop_in_signatures_are_c_abi():
     # extern "C" names are unmangled; the drop-in pair keeps the reference's
     # argument list (wrapper/similarity_transform.cpp:3-37)
@@ -163,11 +191,11 @@ def test_deferred_round_without_store_is_rejected_at_m_minus_1():
 
 
 def test_defer_caps_setter():
-    """st_set_defer_caps (workgroups per CU of the deferred launches): bad
+    """(the tuning build, include/st_tuning.h) st_set_defer_caps (workgroups per CU of the deferred launches): bad
     arguments are refused, a value set is returned by the next call (the
     previous one), and the default is restored."""
-    L = _lib.load()
-    assert L.st_set_defer_caps(2, 0, 0, 4) < 0 and "st_set_defer_caps" in _lib.last_error()
+    L = _lib.load_tuning()
+    assert L.st_set_defer_caps(2, 0, 0, 4) < 0 and "st_set_defer_caps" in _lib.last_error(L)
     assert L.st_set_defer_caps(1, 1, 7, 4) < 0
     assert L.st_set_defer_caps(1, 1, 6, 1) < 0
     assert L.st_set_defer_caps(1, 1, 6, 33) < 0
@@ -181,8 +209,8 @@ def test_defer_ntload_setter():
     rounds) and its size classes: bad arguments are refused, the shipped
     masks are the measured ones, a mask set is returned by the
     next call."""
-    L = _lib.load()
-    assert L.st_set_defer_ntload(3, 0) < 0 and "st_set_defer_ntload" in _lib.last_error()
+    L = _lib.load_tuning()
+    assert L.st_set_defer_ntload(3, 0) < 0 and "st_set_defer_ntload" in _lib.last_error(L)
     assert L.st_set_defer_ntload(0, 0x20) < 0 and L.st_set_defer_ntload(0, 0x100) < 0
     assert L.st_defer_ntload_class(8192, 8192, 2) < 0
     assert [L.st_defer_ntload_class(r, c, 1) for r, c in
@@ -210,8 +238,8 @@ def test_every_cache_setter():
     cached blocks) and its size classes: bad arguments are refused, the
     shipped policies are the measured ones, a policy set is
     returned by the next call."""
-    L = _lib.load()
-    assert L.st_set_every_cache(4, 0) < 0 and "st_set_every_cache" in _lib.last_error()
+    L = _lib.load_tuning()
+    assert L.st_set_every_cache(4, 0) < 0 and "st_set_every_cache" in _lib.last_error(L)
     assert L.st_set_every_cache(0, 4) < 0
     assert L.st_every_cache_class(8192, 8192, 2) < 0
     assert [L.st_every_cache_class(r, c, 1) for r, c in
@@ -230,7 +258,7 @@ def test_every_cache_setter():
     assert L.st_set_every_caps(0, 33) < 0
     caps = [L.st_set_every_caps(c, 3) for c in range(4)]
     assert [L.st_set_every_caps(c, caps[c]) for c in range(4)] == [3, 3, 3, 3]
-    assert L.st_set_mfree_shape(4) < 0 and "st_set_mfree_shape" in _lib.last_error()
+    assert L.st_set_mfree_shape(4) < 0 and "st_set_mfree_shape" in _lib.last_error(L)
     assert L.st_set_mfree_shape(2) == 0 and L.st_set_mfree_shape(0) == 2
 
 
@@ -269,7 +297,7 @@ def test_comm_unique_id_addr():
     L = _lib.load()
     uid = ctypes.create_string_buffer(128)
     assert L.st_comm_unique_id_addr(uid, b"127.0.0.1") == 0
-    assert uid.raw[:7] == b"st-rdv1"
+    assert uid.raw[:7] == b"st-rdv2"
     assert socket.inet_ntoa(uid.raw[16:20]) == "127.0.0.1"        # RdvId.addr
     assert struct.unpack(">H", uid.raw[20:22])[0] > 0               # RdvId.port
     assert L.st_comm_unique_id_addr(uid, b"not-an-address") < 0
@@ -413,6 +441,136 @@ def test_comm_rendezvous_eight_processes_without_a_device():
         assert "did not reach" not in lines["ERR"] and "no word" not in lines["ERR"], lines
         if rc0 != 0:
             assert "could not make the RCCL id" in lines["ERR"], lines
+
+
+def _id_addr(raw: bytes):
+    """(IPv4 address, port) a rendezvous id advertises (bytes 16..21)."""
+    import socket
+    return socket.inet_ntoa(raw[16:20]), int.from_bytes(raw[20:22], "big")
+
+
+def test_comm_rendezvous_ignores_stray_connectors():
+    """Connections that never say hello, or send something else, do not
+    delay the ranks' admission (the host used to read hellos
+    one connection at a time, 5 s each): three ranks as threads get past the
+    presence check within a second or two beside two such connectors."""
+    import socket
+    import threading
+    import time
+    L = _lib.load()
+    old = L.st_set_comm_timeout(20.0)
+    try:
+        uid = ctypes.create_string_buffer(128)
+        assert L.st_comm_unique_id(uid) == 0
+        addr = _id_addr(uid.raw)
+        stray = socket.create_connection(addr)
+        noisy = socket.create_connection(addr)
+        noisy.sendall(b"GET / HTTP/1.0\r\n\r\n")
+        res = {}
+
+        def join(r):
+            c = ctypes.c_void_p()
+            res[r] = (L.st_comm_init(ctypes.byref(c), 3, r, uid.raw, 0), _lib.last_error(), c)
+        th = [threading.Thread(target=join, args=(r,)) for r in (1, 2, 0)]
+        t0 = time.time()
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(60)
+        el = time.time() - t0
+        stray.close()
+        noisy.close()
+        assert sorted(res) == [0, 1, 2] and el < 4.0, (el, res)
+        for rc, err, c in res.values():
+            assert "did not reach" not in err and "no word" not in err, err
+            if rc == 0:
+                L.st_comm_destroy(c)
+    finally:
+        L.st_set_comm_timeout(old)
+
+
+_PEER_GIVES_UP = r"""
+import ctypes, sys, time
+sys.path.insert(0, sys.argv[1])
+from eigen_value_amd import _lib
+L = _lib.load()
+L.st_set_comm_timeout(1.0)
+c = ctypes.c_void_p()
+t0 = time.time()
+rc = L.st_comm_init(ctypes.byref(c), 2, 1, bytes.fromhex(sys.argv[2]), 0)
+print("RC", rc, "EL", round(time.time() - t0, 2))
+print("ERR", _lib.last_error(), flush=True)
+"""
+
+
+def test_comm_rendezvous_host_after_the_peers_deadline():
+    """a peer that gave up at its own deadline and
+    closed its socket leaves its hello in the listen backlog; the id's host,
+    arriving later, must not count it as present (that used to send the
+    RCCL id to a dead rank and enter RCCL without it).  Here the host joins
+    after the peer exited: it names rank 1 as missing (it hung up after its
+    hello) and never gets as far as making the RCCL id."""
+    import sys
+    import time
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id(uid) == 0
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", _PEER_GIVES_UP, repo, uid.raw.hex()],
+                         capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "RC -1" in out.stdout, out.stdout
+    time.sleep(0.5)
+    old = L.st_set_comm_timeout(2.0)
+    try:
+        comm = ctypes.c_void_p()
+        t0 = time.time()
+        rc = L.st_comm_init(ctypes.byref(comm), 2, 0, uid.raw, 0)
+        err, el = _lib.last_error(), time.time() - t0
+    finally:
+        L.st_set_comm_timeout(old)
+    assert rc < 0 and comm.value is None
+    assert "rank 1 of 2 did not reach st_comm_init" in err, err
+    assert "hung up after arriving: 1" in err and "could not make the RCCL id" not in err, err
+    assert el < 8.0
+
+
+def test_comm_id_release():
+    """st_comm_id_release closes the listener of an id its maker will not
+    join: 0 the first time, 1 after; a peer can no longer
+    connect; a foreign id is refused."""
+    import socket
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id_addr(uid, b"127.0.0.1") == 0
+    addr = _id_addr(uid.raw)
+    assert addr[0] == "127.0.0.1"
+    socket.create_connection(addr, timeout=2).close()          # listening
+    assert L.st_comm_id_release(uid.raw) == 0
+    assert L.st_comm_id_release(uid.raw) == 1
+    with pytest.raises(OSError):
+        socket.create_connection(addr, timeout=2)
+    assert L.st_comm_id_release(b"\1" * 128) < 0
+
+
+def test_comm_listener_binds_the_advertised_address():
+    """the listener of an id advertising 127.0.0.1 listens on
+    the loopback address only, not on every interface."""
+    import socket
+    L = _lib.load()
+    uid = ctypes.create_string_buffer(128)
+    assert L.st_comm_unique_id_addr(uid, b"127.0.0.1") == 0
+    port = _id_addr(uid.raw)[1]
+    try:
+        others = {a[4][0] for a in socket.getaddrinfo(socket.gethostname(), None, socket.AF_INET)}
+    except OSError:
+        others = set()
+    others = [a for a in others if not a.startswith("127.")]
+    for a in others:
+        with pytest.raises(OSError):
+            socket.create_connection((a, port), timeout=2)
+    socket.create_connection(("127.0.0.1", port), timeout=2).close()
+    assert L.st_comm_id_release(uid.raw) == 0
 
 
 def test_rccl_version_is_reported():

@@ -1,6 +1,7 @@
 """GPU parity at the BASELINE full sizes against the CPU oracle (not only
-through size-independent properties), and the multi-device paths at every
-device count the box has.
+through size-independent properties), and the communicator's deadline and
+failure paths on one device (the multi-device tests are in
+tests/test_zz_multi_device.py, which collects last).
 
 Tolerances (as tests/test_gpu_parity.py):
   * fp64 vs the oracle's same-semantics solve: iteration count equal, λ
@@ -15,7 +16,6 @@ committed pins (tests/golden/large_oracle.json, make_large_oracle.py) bit
 for bit; 65536² (32 GiB) is checked against the committed pin only.
 """
 import os
-import socket
 
 import numpy as np
 import pytest
@@ -117,184 +117,6 @@ def test_config3_sharded_p1_vs_oracle():
     sh.close()
     del sh, v
     _free()
-
-
-# ---------------------------------------------------------------------------
-# P = 2, 4 and every device the box has (8 on the driver's node); on a box
-# with fewer devices those counts stay collected, skipped, with P in the id
-# ---------------------------------------------------------------------------
-def _multi_counts():
-    """P in {2, 4, NDEV} (and 8, the driver's node) ∩ [2, NDEV]; counts the
-    box lacks are skipped params whose id names the count."""
-    out = []
-    for p in sorted({2, 4, 8} | ({NDEV} if NDEV > 1 else set())):
-        if p <= NDEV and (p in (2, 4) or p == NDEV):
-            out.append(pytest.param(p, id=f"P{p}"))
-        elif p > NDEV:
-            out.append(pytest.param(p, id=f"P{p}-skipped-needs-{p}-devices",
-                                    marks=pytest.mark.skip(reason=f"needs >= {p} HIP devices, "
-                                                                  f"this box has {NDEV}")))
-    return out
-
-
-def _device_counts():
-    return [pytest.param(1, id="P1")] + _multi_counts()
-
-
-@pytest.mark.parametrize("ngpus", _device_counts())
-def test_native_multi_gpu_all_devices(orc, ngpus):
-    """st_solve_multi_* over `ngpus` devices (ncclCommInitAll, one grouped
-    all-gather per round) vs the oracle: a k_round block size (3001, the
-    oracle run here) and a flat-round (deferred-write) block size (32768²
-    random fp64 seed 0, 32768/P rows per device, vs the committed oracle pin
-    tests/golden/large_oracle.json: no host oracle at full size)."""
-    from eigen_value_amd.multi import solve_multi
-    n = 3001
-    ref = orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL, nthreads=HOST_THREADS)
-    lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=3)
-    assert it == ref.iter_count and st["rounds"] == ref.rounds_evaluated, n
-    assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
-    assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
-    r2 = solve_multi(n, "random", ngpus=ngpus, seed=3, write_every_round=True)
-    assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
-    pin, v_pin = large_oracle("random32768_f64")
-    n = 32768
-    lam, v, it, st = solve_multi(n, "random", ngpus=ngpus, seed=0)
-    assert it == pin["iter_count"] == 3 and st["rounds"] == pin["rounds_evaluated"]
-    assert abs(lam - pin["eigen_val"]) <= 1e-10 * pin["eigen_val"]
-    assert np.max(np.abs(v - v_pin)) <= 1e-10
-    r2 = solve_multi(n, "random", ngpus=ngpus, seed=0, write_every_round=True)
-    assert r2[0] == lam and r2[2] == it and np.array_equal(r2[1], v)
-    del v, r2
-    _free()
-
-
-def _comm_worker(rank, world, port, outdir):
-    import torch.distributed as dist
-    from eigen_value_amd.sharded import RcclComm, ShardedSimilarityTransform
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world,
-                            device_id=torch.device("cuda", rank))
-    try:
-        rc = RcclComm()
-        info = rc.info()
-        for dt in (torch.float64, torch.float32):
-            out = torch.full((world * 5,), -1.0, dtype=dt, device="cuda")
-            out[rank * 5:(rank + 1) * 5] = torch.arange(rank * 5, rank * 5 + 5, dtype=dt)
-            rc.allgather(out, out[rank * 5:(rank + 1) * 5])
-            torch.cuda.synchronize()
-            assert torch.equal(out.cpu(), torch.arange(world * 5, dtype=dt))
-        rc.close()
-        res = []
-        for n in (3001, 9216):       # k_round and flat (deferred) blocks
-            sh = ShardedSimilarityTransform(n, torch.float64, comm="native")
-            assert sh.rccl is not None
-            sh.load("random", seed=3)
-            lam, v, it, rounds = sh.solve()
-            sh.close()
-            res += [lam, it, rounds]
-            if rank == 0:
-                np.save(os.path.join(outdir, f"v{n}.npy"), v.cpu().numpy())
-        np.save(os.path.join(outdir, f"r{rank}.npy"),
-                np.array([info["nranks"], info["rank"], info["device"], *res]))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", _multi_counts())
-def test_library_comm_all_devices(tmp_path, orc, world):
-    """The library-owned RCCL communicator (st_comm_*) with nranks = every
-    device: RCCL reports that many ranks, the in-slot all-gather is right,
-    and the one-process-per-GPU sharded solve matches the oracle."""
-    import torch.multiprocessing as mp
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    mp.spawn(_comm_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
-    refs = [orc.similarity_transform(orc.random_matrix(n, 3), orc.SEM_SYCL,
-                                     nthreads=HOST_THREADS) for n in (3001, 9216)]
-    for r in range(world):
-        got = np.load(tmp_path / f"r{r}.npy")
-        assert tuple(int(x) for x in got[:3]) == (world, r, r)
-        for j, n in enumerate((3001, 9216)):
-            ref = refs[j]
-            lam, it, rounds = got[3 + 3 * j:6 + 3 * j]
-            assert int(it) == ref.iter_count and int(rounds) == ref.rounds_evaluated
-            assert abs(lam - ref.eigen_val) <= 1e-10 * ref.eigen_val
-            if r == 0:
-                v = np.load(tmp_path / f"v{n}.npy")
-                assert np.max(np.abs(v - ref.eigen_vec)) <= 1e-10
-
-
-# ---------------------------------------------------------------------------
-# configs[3] itself: 65536² random fp64 (seed 0) row-block sharded over
-# every device of the box with one RCCL all-gather per round, against the
-# committed oracle pin (no host oracle run: 32 GiB; the pin is the streaming
-# oracle's solve, bit-identical to the plain loop)
-# ---------------------------------------------------------------------------
-def _check_config3(lam, v, it, rounds):
-    pin, v_pin = large_oracle("random65536_f64")
-    assert it == pin["iter_count"] == 3 and rounds == pin["rounds_evaluated"]
-    assert abs(lam - pin["eigen_val"]) <= 1e-10 * pin["eigen_val"]
-    assert np.max(np.abs(np.asarray(v) - v_pin)) <= 1e-10
-
-
-@pytest.mark.parametrize("ngpus", _device_counts())
-def test_config3_native_multi_gpu_vs_pin(ngpus):
-    """BASELINE configs[3] through st_solve_multi_f64 (one process, `ngpus`
-    devices, non-blocking RCCL communicators, one grouped ncclAllGather per
-    round; gen_kind 2: every device generates its own 65536/ngpus rows),
-    vs the oracle pin: iterations 3, λ and v to 1e-10.  ngpus = 1 runs here;
-    the all-device case runs where the box has them (similarity_transform.cpp:39-53)."""
-    from eigen_value_amd.multi import solve_multi
-    lam, v, it, st = solve_multi(65536, "random", ngpus=ngpus, seed=0)
-    _check_config3(lam, v, it, st["rounds"])
-    del v
-    _free()
-
-
-def _config3_worker(rank, world, port, outdir):
-    import torch.distributed as dist
-    from eigen_value_amd.sharded import ShardedSimilarityTransform
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    torch.cuda.set_device(rank)
-    dist.init_process_group("nccl", rank=rank, world_size=world,
-                            device_id=torch.device("cuda", rank))
-    try:
-        sh = ShardedSimilarityTransform(65536, torch.float64, comm="native")
-        info = sh.rccl.info()
-        sh.load("random", seed=0)
-        lam, v, it, rounds = sh.solve()
-        sh.close()
-        if rank == 0:
-            np.save(os.path.join(outdir, "v.npy"), v.cpu().numpy())
-        np.save(os.path.join(outdir, f"r{rank}.npy"),
-                np.array([info["nranks"], info["rank"], info["device"], lam, it, rounds,
-                          sh.part.nrows, info["rccl_version_code"]]))
-    finally:
-        dist.destroy_process_group()
-
-
-@pytest.mark.parametrize("world", _multi_counts())
-def test_config3_one_process_per_gpu_vs_pin(tmp_path, world):
-    """BASELINE configs[3] as the driver's scaling run shards it: one process
-    per GPU (mp.spawn), ShardedSimilarityTransform(comm="native") - the
-    library's RCCL communicator, 65536/world rows per rank, deferred writes -
-    vs the oracle pin; RCCL reports `world` ranks on distinct devices."""
-    import torch.multiprocessing as mp
-    with socket.socket() as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
-    mp.spawn(_config3_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
-    devices = set()
-    for r in range(world):
-        nranks, rk, device, lam, it, rounds, nrows, rccl = np.load(tmp_path / f"r{r}.npy")
-        assert (int(nranks), int(rk)) == (world, r) and int(nrows) == 65536 // world
-        assert int(rccl) >= 22000         # the RCCL the ranks' library calls bound to
-        devices.add(int(device))
-        _check_config3(float(lam), np.load(tmp_path / "v.npy"), int(it), int(rounds))
-    assert len(devices) == world
 
 
 # ---------------------------------------------------------------------------

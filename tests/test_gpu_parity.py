@@ -368,6 +368,34 @@ def test_sharded_single_gpu_matches_device_solver(solver, n):
     assert torch.equal(v, v2)
 
 
+@pytest.mark.parametrize("n,mf", [(3000, False), (8192, False), (8192, True), (2048, True)])
+def test_sharded_rounds_fast_path_bitwise(n, mf):
+    """sh.rounds(K) (pre-resolved launches, the bench's timed loop) enqueues
+    exactly what K calls of sh.round() do: matrix, row sums, v and state
+    bitwise, on the one-launch round, the flat round and the matrix-free
+    form, including the gated rounds past a stop."""
+    from eigen_value_amd.sharded import ShardedSimilarityTransform
+    out = []
+    for fast in (False, True):
+        sh = ShardedSimilarityTransform(n, torch.float64, matrix_free=mf)
+        sh.load("hilbert")
+        sh.start()
+        for eps, k in ((0.0, 5), (1e-3, 30)):          # fixed rounds, then a stop
+            if fast:
+                sh.rounds(k, eps, 100)
+            else:
+                for _ in range(k):
+                    sh.round(eps, 100)
+        torch.cuda.synchronize()
+        out.append((sh.mat.clone(), [x.clone() for x in sh.s], [x.clone() for x in sh.vb],
+                    dev.read_state(sh.state), sh.k, sh.cur))
+        sh.close()
+    a, b = out
+    assert torch.equal(a[0], b[0]) and a[3] == b[3] and a[4:] == b[4:]
+    assert all(torch.equal(x, y) for x, y in zip(a[1] + a[2], b[1] + b[2]))
+    assert a[3]["done"] == 1
+
+
 @pytest.mark.parametrize("kw", [dict(eps=1e-3), dict(eps=0.0, max_itr=7), dict(eps=0.0, max_itr=9)])
 def test_sharded_deferred_writes_bitwise(kw):
     """The sharded driver's solve with deferred writes (the default on flat
@@ -1205,184 +1233,6 @@ def test_deferred_writes_bitwise(solver, dt, n, sem):
                (r2[0], r2[2], r2[3]["rounds"], r2[3]["converged"]), kw
         assert torch.equal(r1[1], r2[1]), kw                # v bitwise
         assert torch.equal(a1, a2), kw                      # final matrix bitwise
-
-
-@pytest.mark.parametrize("dt,n", [(np.float64, 4352), (np.float64, 16385),
-                                  (np.float32, 6144), (np.float32, 23171)])
-def test_deferred_caps_do_not_change_results(solver, dt, n):
-    """The workgroups-per-CU caps of the deferred launches (st_set_defer_caps,
-    dynamic LDS reserved per workgroup) change residency only: a solve under
-    the shipped table, with every cap removed and with every slot at 2 / 8
-    per CU is bit-identical (λ, v, iterations, final matrix)."""
-    L = _lib.load()
-    d = 1 if dt == np.float64 else 0
-    nt = 1 if n * n * np.dtype(dt).itemsize >= (2 << 30) else 0
-    base = dev.generate("random", n, TD[dt], seed=8, device=DEV)
-    slots = (0, 1, 2, 3, 4, 6)
-    saved = {sl: L.st_set_defer_caps(d, nt, sl, 0) for sl in slots}     # read + clear
-    try:
-        for sl in slots:
-            L.st_set_defer_caps(d, nt, sl, saved[sl])                   # shipped table
-        out = []
-        for cap in (None, 0, 2, 8):
-            if cap is not None:
-                for sl in slots:
-                    assert L.st_set_defer_caps(d, nt, sl, cap) >= 0
-            a = base.clone()
-            r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
-            out.append((r[0], r[2], r[1].cpu(), a))
-        for o in out[1:]:
-            assert o[0] == out[0][0] and o[1] == out[0][1]
-            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
-    finally:
-        for sl in slots:
-            L.st_set_defer_caps(d, nt, sl, saved[sl])
-
-
-@pytest.mark.parametrize("n", [4352, 8192, 10240])
-def test_deferred_ntload_does_not_change_results(solver, n):
-    """Non-temporal matrix loads in the cached fp64 deferred rounds
-    (st_set_defer_ntload, per block size class) change the cache policy
-    only: a solve under the shipped mask, with cached loads throughout, with
-    every round's loads non-temporal and with the storing round's stores
-    non-temporal too (bit 7) is bit-identical (λ, v, iterations, final
-    matrix)."""
-    L = _lib.load()
-    cls = L.st_defer_ntload_class(n, n, 1)
-    assert cls == {4352: 0, 8192: 1, 10240: 2}[n]
-    base = dev.generate("random", n, torch.float64, seed=9, device=DEV)
-    saved = L.st_set_defer_ntload(cls, 0)
-    try:
-        out = []
-        for mask in (saved, 0, 0x5f, 0xdf):
-            assert L.st_set_defer_ntload(cls, mask) >= 0
-            a = base.clone()
-            r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
-            out.append((r[0], r[2], r[1].cpu(), a))
-        for o in out[1:]:
-            assert o[0] == out[0][0] and o[1] == out[0][1]
-            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
-    finally:
-        L.st_set_defer_ntload(cls, saved)
-
-
-@pytest.mark.parametrize("n,dtype", [(8192, "f32"), (16384, "f64"), (23200, "f32")])
-def test_deferred_cache_flip_does_not_change_results(solver, n, dtype):
-    """The deferred rounds' cache policy on the other forms
-    (st_set_defer_cache: cached fp32 blocks, and the non-temporal form from
-    2 GiB, whose loads / stores a mask turns cached) moves no result: λ, v,
-    iterations and the final matrix are bit-identical under every mask."""
-    L = _lib.load()
-    d = 1 if dtype == "f64" else 0
-    dt = torch.float64 if d else torch.float32
-    cls = L.st_every_cache_class(n, n, d)
-    assert cls == {8192: 0, 16384: 3, 23200: 3}[n]
-    base = dev.generate("random", n, dt, seed=12, device=DEV)
-    saved = L.st_set_defer_cache(d, cls, 0)
-    try:
-        out = []
-        for mask in (saved, 0x1f, 0x41, 0xdf):
-            assert L.st_set_defer_cache(d, cls, mask) >= 0
-            a = base.clone()
-            r = solver.solve(a, inplace=True, eps=0.0, max_itr=9)
-            out.append((r[0], r[2], r[1].cpu(), a))
-        for o in out[1:]:
-            assert o[0] == out[0][0] and o[1] == out[0][1]
-            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
-    finally:
-        L.st_set_defer_cache(d, cls, saved)
-
-
-@pytest.mark.parametrize("n,dtype", [(6144, "f64"), (4608, "f64"), (8192, "f32")])
-def test_mfree_shapes_do_not_change_results(solver, n, dtype):
-    """Every launch shape of the matrix-free round (st_set_mfree_shape:
-    cached 2 / 4 rows per group, non-temporal 4 rows, the table) gives the
-    same solve bit for bit (λ, v, iterations): the rows a workgroup takes
-    change no row's summation order."""
-    L = _lib.load()
-    dt = torch.float64 if dtype == "f64" else torch.float32
-    a = dev.generate("random", n, dt, seed=14, device=DEV)
-    saved = L.st_set_mfree_shape(0)
-    try:
-        out = []
-        for shape in (0, 1, 2, 3):
-            assert L.st_set_mfree_shape(shape) >= 0
-            r = solver.solve(a, matrix_free=True, eps=0.0, max_itr=7)
-            out.append((r[0], r[2], r[1].cpu()))
-        for o in out[1:]:
-            assert o[0] == out[0][0] and o[1] == out[0][1] and torch.equal(o[2], out[0][2])
-    finally:
-        L.st_set_mfree_shape(saved)
-
-
-@pytest.mark.parametrize("n", [4352, 8192, 10240])
-def test_every_cache_does_not_change_results(solver, n):
-    """The every-round flat launch's cache policy (st_set_every_cache: the
-    loads', the stores' or both policies turned over, per block size class)
-    changes where lines are kept only: a solve that stores every round is
-    bit-identical under every policy (λ, v, iterations, final matrix)."""
-    L = _lib.load()
-    cls = L.st_every_cache_class(n, n, 1)
-    assert cls == {4352: 0, 8192: 1, 10240: 2}[n]
-    base = dev.generate("random", n, torch.float64, seed=11, device=DEV)
-    saved = L.st_set_every_cache(cls, 0)
-    try:
-        out = []
-        # (policy, piece tile, workgroups per CU): st_set_every_tile and
-        # st_set_every_caps are for tools, and move no result either
-        for pol, tile, cap in ((saved, 0, 0), (0, 0, 0), (1, 0, 0), (2, 0, 0), (3, 0, 0),
-                               (saved, 1, 0), (saved, 16, 3)):
-            assert L.st_set_every_cache(cls, pol) >= 0
-            assert L.st_set_every_tile(cls, tile) >= 0 and L.st_set_every_caps(cls, cap) >= 0
-            a = base.clone()
-            r = solver.solve(a, inplace=True, eps=0.0, max_itr=7, write_every_round=True)
-            out.append((r[0], r[2], r[1].cpu(), a))
-        for o in out[1:]:
-            assert o[0] == out[0][0] and o[1] == out[0][1]
-            assert torch.equal(o[2], out[0][2]) and torch.equal(o[3], out[0][3])
-    finally:
-        L.st_set_every_cache(cls, saved)
-        L.st_set_every_tile(cls, 0)
-        L.st_set_every_caps(cls, 0)
-
-
-@pytest.mark.parametrize("limit", [8, 1000, 4096])
-def test_flat_2d_grid_bitwise(solver, orc, limit):
-    """A flat launch of more workgroups than one dispatch dimension holds
-    (2^32 - 1 work-items: fp64 from 131072², test_max_single_gpu_size) goes
-    2-D.  Forced 2-D at small sizes (st_set_flat_grid_limit; widths that
-    divide the grid and ones that leave padding workgroups) every launch
-    form - the every-round and deferred solves, the two split halves - is
-    bit-identical to the 1-D grid."""
-    n = 4352                                                  # 144.5 MiB: flat
-    base = dev.generate("random", n, torch.float64, seed=6, device=DEV)
-    a = orc.random_matrix(6000, 3, np.float64, nrows=2049)    # split block
-    s_full = torch.from_numpy(orc.random_matrix(6000, 9, np.float64, nrows=1)[0] + 0.5).to(DEV)
-
-    def run():
-        out = []
-        for every in (False, True):
-            m = base.clone()
-            r = solver.solve(m, inplace=True, eps=0.0, max_itr=5, write_every_round=every)
-            out += [r[0], r[2], r[1].cpu(), m]
-        ta, tv = torch.from_numpy(a).to(DEV), torch.ones(6000, dtype=torch.float64, device=DEV)
-        s_next = torch.empty(2049, dtype=torch.float64, device=DEV)
-        part = dev.split_flat_scratch(2049, 6000, 3000, 5049, torch.float64, DEV)
-        state = dev.new_state(DEV)
-        for span in (dev.SPAN_LOCAL, dev.SPAN_REMOTE):
-            dev.split_flat_round(ta, s_full, s_next if span == dev.SPAN_REMOTE else None,
-                                 part, tv if span == dev.SPAN_REMOTE else None, state,
-                                 span=span, row0=3000, col0=3000, col1=5049, eps=1e-3, k=1)
-        return out + [ta, s_next, tv, dev.read_state(state)]
-
-    ref = run()
-    try:
-        assert dev.set_flat_grid_limit(limit) == limit
-        got = run()
-    finally:
-        assert dev.set_flat_grid_limit(0) == 16777208
-    for x, y in zip(ref, got):
-        assert (torch.equal(x, y) if isinstance(x, torch.Tensor) else x == y)
 
 
 def test_max_single_gpu_size(solver):

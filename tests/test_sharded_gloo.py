@@ -595,16 +595,20 @@ def test_library_comm_is_used_only_if_every_rank_has_one(tmp_path, fail_rank):
 
 
 # ---------------------------------------------------------------------------
-# the library communicator's presence check (sharded.rendezvous): over the
-# group's c10d store, before any rank enters RCCL
+# the library communicator's presence check: group rank 0 hands the id over
+# the group's c10d store, st_comm_init's rendezvous (st_rendezvous.hip) then
+# checks every rank before any enters RCCL (one presence
+# layer since round 6)
 # ---------------------------------------------------------------------------
 def _rdv_worker(rank, world, port, stall_rank, outdir):
+    import json
     import time
 
     from eigen_value_amd import sharded
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dist.barrier()            # every rank's mesh is up before one of them moves on
+    _lib.load().st_set_comm_timeout(2.0)
     res = {"rank": rank}
     try:
         if rank == stall_rank:
@@ -612,48 +616,52 @@ def _rdv_worker(rank, world, port, stall_rank, outdir):
         else:
             t0 = time.time()
             try:
-                res["payload"] = sharded.rendezvous(
-                    None, 2.0,
-                    payload_from_first=lambda hosts: f"id-bytes {len(hosts)}".encode()).decode()
+                comm, err = sharded.make_comm_agreed(
+                    None, lambda: sharded.RcclComm(None, device_index=0))
+                res["comm"] = comm is not None
+                res["err"] = err
+                if comm is not None:
+                    comm.close()
             except sharded.PeerMissingError as e:
                 res.update(missing=e.missing, msg=str(e))
             res["el"] = time.time() - t0
-            # a second rendezvous on the same group (the next communicator)
-            # is matched by order and does not see the first one's keys
-            if stall_rank < 0:
-                def boom(hosts):
-                    raise RuntimeError("no id today")
-                try:
-                    sharded.rendezvous(None, 5.0, payload_from_first=boom)
-                except _lib.EigenValueError as e:
-                    res["second"] = str(e)
-        import json
         with open(os.path.join(outdir, f"rdv{rank}.json"), "w") as f:
             json.dump(res, f)
-        dist.barrier()        # rank 0 hosts the store: nobody leaves before all are done
+        if stall_rank < 0:
+            dist.barrier()    # rank 0 hosts the store: nobody leaves before all are done
+        else:
+            time.sleep(7.0 if rank == 0 else 0.0)
     finally:
-        dist.destroy_process_group()
+        if stall_rank < 0:
+            dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("stall_rank", [-1, 1])
-def test_rendezvous_names_the_missing_rank(tmp_path, stall_rank):
-    """gloo world 3.  All present: every rank returns group rank 0's payload
-    (the library id), and a payload failure reaches every rank as an error.
-    Rank 1 absent: ranks 0 and 2 raise PeerMissingError naming rank 1 within
-    the 2 s deadline (not after a hang in RCCL init or torch's broadcast)."""
+@pytest.mark.parametrize("stall_rank", [-1, 1, 0])
+def test_communicator_rendezvous_names_the_missing_rank(tmp_path, stall_rank):
+    """gloo world 3 through RcclComm / make_comm_agreed, as a sharded solve
+    takes the library communicator.  All present: every rank passes the
+    presence check and gets as far as the RCCL id (which needs a device: on
+    CPU every rank reports that, none a missing rank).  Rank 1 absent: ranks
+    0 and 2 raise PeerMissingError naming rank 1 within the 2 s deadline,
+    from st_comm_init's rendezvous, with no rank in RCCL.  Rank 0 (the id's
+    maker) absent: ranks 1 and 2 raise PeerMissingError naming rank 0 from
+    the id hand-over, at the same deadline."""
     import json
     mp.spawn(_rdv_worker, args=(3, _free_port(), stall_rank, str(tmp_path)), nprocs=3,
              join=True)
     for r in range(3):
-        res = json.load(open(tmp_path / f"rdv{r}.json"))
         if r == stall_rank:
             continue
+        res = json.load(open(tmp_path / f"rdv{r}.json"))
         if stall_rank < 0:
-            assert res["payload"] == "id-bytes 3" and res["el"] < 5.0
-            assert "group rank 0 failed: RuntimeError: no id today" in res["second"]
+            assert "missing" not in res, res
+            assert res["comm"] or "could not make the RCCL id" in res["err"], res
+        elif stall_rank == 1:
+            assert "RCCL rank 1 of 3 did not reach st_comm_init" in res["msg"], res
+            assert "no rank entered RCCL" in res["msg"] and 1.9 <= res["el"] < 5.5, res
         else:
-            assert res["missing"] == [1], res
-            assert "group rank 1 of 3 did not reach the communicator rendezvous" in res["msg"]
+            assert res["missing"] == [0], res
+            assert "group rank 0 of 3 did not hand over the communicator id" in res["msg"]
             assert 1.9 <= res["el"] < 5.5, res
 
 

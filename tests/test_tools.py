@@ -1,5 +1,5 @@
 """CPU: the measurement tools' arithmetic (tools/pmc_traffic.py,
-tools/sweep_table.py) on synthetic rocprofv3 / sweep output."""
+tools/defer_profile.py, tools/check_citations.py) on synthetic rocprofv3 output."""
 import csv
 import json
 import os
@@ -52,22 +52,6 @@ def test_pmc_traffic_corrections(tmp_path):
     assert abs(e["k_round"]["trace_ms_avg"] - 0.1) < 1e-12
     assert abs(e["k_mfree"]["traffic_over_algorithmic"] - 1.0) < 1e-12
     assert d["fused_bytes_per_launch"] == e["k_round"]["hbm_bytes_per_launch"]
-
-
-def test_sweep_table(tmp_path):
-    log = tmp_path / "s.log"
-    log.write_text(
-        "n=2048 f64  matrix 0.031 GiB\n"
-        "  k_round rows=2 nt=0 alt=1 grid= 256    0.0100 ms   1.0 GB/s\n"
-        "  k_round rows=4 nt=0 alt=1 grid= 256    0.0200 ms   1.0 GB/s\n"
-        "n=1024x4096 f32  block 0.016 GiB\n"
-        "  k_round rows=2 nt=0 alt=1 grid= 256    0.0050 ms   1.0 GB/s\n"
-        "  k_mfree rows=4 nt=1 alt=1 grid= 512    0.0040 ms   1.0 GB/s\n")
-    out = subprocess.run([sys.executable, os.path.join(TOOLS, "sweep_table.py"), str(log)],
-                         check=True, capture_output=True, text=True).stdout
-    assert "1024x4096 32" in out and "2048 64" in out
-    row = [ln for ln in out.splitlines() if ln.startswith("(4, 0, 1, 256)")][0]
-    assert "2.000" in row
 
 
 def _kflat(np_, store):

@@ -10,7 +10,8 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 D=$ROOT/tools/asan
 if [ "${1:-run}" = build ]; then
   mkdir -p $D
-  FL="--offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off -I$ROOT/include -I$ROOT/eigen_value_amd/csrc"
+  # the tuning build's ABI (-DST_TUNING_ABI=1): the driver checks the setters too
+  FL="--offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -ffp-contract=off -DST_TUNING_ABI=1 -I$ROOT/include -I$ROOT/eigen_value_amd/csrc"
   SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host -fno-omit-frame-pointer"
   for f in st_kernels st_solve st_multi st_rendezvous; do
     /opt/rocm/bin/hipcc $FL $SAN -c $ROOT/eigen_value_amd/csrc/$f.hip -o $D/$f.o &
