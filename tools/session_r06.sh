@@ -15,6 +15,12 @@ new)
   # this round's new paths first (flat K0, traced solves): a failure ends the session
   timeout -k 10 400 python3 -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_parity.py -k "rowsum or trace or fp32_random_at_reference_eps or fuzz or flat_round_vs_round or deferred_writes_bitwise or sharded_single_gpu or native_multi_gpu_flat" > $O/new.log 2>&1; rc=$?
   tail -25 $O/new.log; [ $rc -eq 0 ] || fail new $rc ;;
+new2)
+  # session 2's changes first: the fast round path, the tuning build, the
+  # one-GPU rehearsals of the multi-device workers, the communicator probes
+  timeout -k 10 900 python3 -u -m pytest -x -v --timeout 600 --timeout-method thread -m gpu tests/test_gpu_parity.py tests/test_gpu_tuning.py tests/test_zz_multi_device.py tests/test_gpu_fullsize.py -k "fast_path or tuning or rehearsal or comm_init or grouped_init or trace or rowsum" > $O/new2.log 2>&1; rc=$?
+  tail -30 $O/new2.log; [ $rc -eq 0 ] || fail new2 $rc ;;
+collect) python3 -m pytest --collect-only -q -m gpu tests/ > $O/collect.log 2>&1; tail -25 $O/collect.log ;;
 tests) run pytest_gpu 900 python3 -u -m pytest -x -q -rs --timeout 300 --timeout-method thread -m gpu tests/; tail -15 $O/pytest_gpu.log ;;
 smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -3 $O/smoke.log ;;
 fuzz) run fuzz 900 python3 -u tools/fuzz_parity.py --cases ${FUZZ_CASES:-300} --seed ${FUZZ_SEED:-20261201} --json $O/r06_fuzz_parity.json; tail -3 $O/fuzz.log; grep -c STRADDLE $O/fuzz.log ;;
