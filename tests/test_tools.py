@@ -54,10 +54,27 @@ def test_pmc_traffic_corrections(tmp_path):
     assert d["fused_bytes_per_launch"] == e["k_round"]["hbm_bytes_per_launch"]
 
 
-def _kflat(np_, store):
-    # k_flat's template arguments as rocprofv3 prints them (NP is the 12th)
-    return ("void st::dev::k_flat<double, 2, 0, true, 8, false, true, 2, 256, 0, 1, "
-            f"{np_}, 1, false, {1 if store else 0}>(double*, double const*)")
+def _kflat(np_, store, old=False):
+    # k_flat's template arguments as rocprofv3 prints them: NP is the 9th
+    # (round 6 on), the 12th in earlier rounds' traces (BLK = 256 the 9th)
+    if old:
+        return ("void st::dev::k_flat<double, 2, 0, true, 8, false, true, 2, 256, 0, 1, "
+                f"{np_}, 1, false, {1 if store else 0}>(double*, double const*)")
+    return ("void st::dev::k_flat<double, 2, 0, true, 8, true, 2, 0, "
+            f"{np_}, 1, {1 if store else 0}>(double*, double const*)")
+
+
+def test_kflat_np_parsed_in_both_layouts():
+    sys.path.insert(0, TOOLS)
+    import defer_profile
+    import pmc_traffic
+    for old in (False, True):
+        for np_ in (0, 3, 5):
+            name = _kflat(np_, np_ == 5, old)
+            assert pmc_traffic.flat_np(name) == np_
+            assert defer_profile.np_of(name) == np_
+    assert pmc_traffic.flat_np("void st::dev::k_flat<double, 2, 0, true, 1, true, 2, 0, -1, "
+                               "2, -1, false, 2>(double*)") == -1
 
 
 def test_defer_profile_cycle_and_launch_rows(tmp_path):

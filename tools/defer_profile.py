@@ -248,7 +248,9 @@ def np_of(name):
     """k_flat's last template argument: -1 = stores every round, else the
     number of pending rounds it re-applies (its position in the group)."""
     m = re.search(r"k_flat<([^>]*)>", name)
-    return int(m.group(1).split(",")[11])
+    args = m.group(1).split(",")
+    # before round 6 the 9th argument was BLK (256) and NP the 12th
+    return int(args[11 if len(args) > 11 and args[8].strip() == "256" else 8])
 
 
 def summarise(path, n, elem, m, workload, events=None, launches=None, block_rows=None):

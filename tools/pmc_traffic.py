@@ -28,10 +28,13 @@ import statistics
 
 
 def flat_np(name):
-    """k_flat's NP template argument (the 12th): -1 = the every-round
-    transform, else the pending rounds a deferred-write launch re-applies."""
+    """k_flat's NP template argument: -1 = the every-round transform, else
+    the pending rounds a deferred-write launch re-applies (the 9th template
+    argument since round 6; the 12th, after BLK = 256 as the 9th, in
+    earlier rounds' traces)."""
     args = name.split("(")[0].split("<", 1)[1].rsplit(">", 1)[0].split(",")
-    return int(args[11]) if len(args) > 11 else -1
+    i = 11 if len(args) > 11 and args[8].strip() == "256" else 8   # old: BLK = 256 there
+    return int(args[i]) if len(args) > i else -1
 
 
 def short(name):
@@ -73,7 +76,8 @@ def main():
     write = load_seq(a.write, lambda r: float(r["Counter_Value"]))
     trace = load_seq(a.trace, lambda r: (int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
                      * 1e-6) if a.trace else {}
-    algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb}
+    algo = {"k_round": 2.0 * nb, "k_flat": 2.0 * nb, "k_mfree": nb, "k_fused": nb,
+            "k_flat_sum": nb}   # k_flat_sum: K0 in the flat form (round 6)
     for npend in range(m):
         algo[f"k_flat_np{npend}"] = nb
         algo[f"k_flat_np{npend}_store"] = 2.0 * nb

@@ -36,5 +36,22 @@ k0)
   D=$O/k0; mkdir -p $D
   run k0 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 tools/k0_probe.py
   cat $O/k0.log | tail -12; head -12 $D/run_kernel_stats.csv ;;
+sync)
+  # the host clock's fixed start / stop latency
+  run sync_default 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_default.json; tail -6 $O/sync_default.log
+  HSA_ENABLE_INTERRUPT=0 run sync_polling 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_polling.json; tail -6 $O/sync_polling.log ;;
+pmc)
+  # kernel trace + FETCH_SIZE / WRITE_SIZE passes of the bench's own legs
+  # for the headline workload and the north star (fp64, fp32), one process
+  # each (--strong: no weak-scaled rank blocks in the same trace)
+  for W in "hilbert 8192 f64" "random 32768 f64" "random 32768 f32"; do
+    set -- $W; K=$1; N=$2; T=$3; WL=$K${N}_$T; D=$O/pmc_$WL; mkdir -p $D
+    A="bench.py --n $N --kind $K --dtype $T --strong --no-cpu --no-north-star --no-headline --no-configs3 --steps 20 --warmup 5"
+    run prof_$WL 600 rocprofv3 --kernel-trace --stats --output-format csv -d $D/prof -o run -- python3 $A
+    run fetch_$WL 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o run -- python3 $A
+    run write_$WL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/write -o run -- python3 $A
+    EL=8; [ $T = f32 ] && EL=4; DT=double; [ $T = f32 ] && DT=float
+    python3 tools/pmc_traffic.py --workload $WL --n $N --elem $EL --dtype $DT --fetch $D/fetch/run_counter_collection.csv --write $D/write/run_counter_collection.csv --trace $D/prof/run_kernel_trace.csv --out $O/r06_${WL}_pmc.json | tee -a $O/pmc_summary.log
+  done ;;
 *) echo "unknown step $step"; exit 2 ;;
 esac; done

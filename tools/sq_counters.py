@@ -23,7 +23,7 @@ def key(name):
     if not m:
         return None
     a = [x.strip() for x in m.group(1).split(",")]
-    return f"k_flat {a[0]} NT={a[3]} R={a[4]} NP={a[11]}"
+    return f"k_flat {a[0]} NT={a[3]} R={a[4]} NP={a[11 if len(a) > 11 and a[8].strip() == "256" else 8]}"
 
 
 def main(paths):
