@@ -394,12 +394,12 @@ def round_distribution(sh, kind, steps, warmup, torch):
     `value`."""
     sh.load(kind)
     cool_down(torch)
+    clk0 = gpu_clocks(torch, torch.cuda.current_device())
     sh.start()
     for _ in range(warmup):
         sh.round(0.0, BIG)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     torch.cuda.synchronize()
-    clk0 = gpu_clocks(torch, torch.cuda.current_device())
     ev[0].record()
     for k in range(steps):
         sh.round(0.0, BIG)
@@ -443,6 +443,11 @@ def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     the timed region runs without events, and a separate pass after it
     brackets each launch with its own pair for the kernel average."""
     cool_down(torch)
+    # the clock levels are read before the warm-up rounds, not at t0: an
+    # amdgpu sysfs clock read asks the SMU, and the launches right after it
+    # start late (tools/sync_probe.py --clocks)
+    if clocks_key:
+        CLOCKS[clocks_key + "_before"] = gpu_clocks(torch, torch.cuda.current_device())
     sh.start()
     sh.rounds(warmup, 0.0, BIG)
     torch.cuda.synchronize()
@@ -450,8 +455,6 @@ def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    if clocks_key:
-        CLOCKS[clocks_key + "_before"] = gpu_clocks(torch, torch.cuda.current_device())
     t0 = time.perf_counter()
     if world == 1:
         ev[0][0].record()

@@ -16,8 +16,13 @@ both traces (the library's ST_FLAG_TRACE_SUMS and the oracle's
 * each solve's stop round must be the first round whose traced s_k passes
   the stop test, computed here in the solve's dtype exactly as the kernels
   and ``orc_stop`` do (self-consistency of the traces);
-* per round, the row sums must agree to ``DEV_ULPS`` ulps of max s_k
-  (measured deviations are 0-8 ulps, ``profiles/r06_fuzz_parity_*.json``);
+* per round k, the row sums must agree to ``DEV_ULPS`` ulps of max s_k
+  for the transform forms (measured: at most 12 in fp32, 8 in fp64 over
+  1800 cases, ``profiles/r06_fuzz_parity_*.json``), and to
+  ``DEV_ULPS + k`` for the matrix-free form, which evaluates
+  s_k = (A_0 x) ⊘ x - a different rounding path from the transform the
+  oracle runs - and drifts from it by up to ~0.6 ulp per round (measured:
+  120 ulps after 200 fp32 rounds);
 * if no round straddles EPS, the two solves stop in the same round (the
   iteration counts are equal); otherwise the first straddling round is
   reported with its margin |max|Δs|_oracle - EPS|, which the measured row
@@ -30,8 +35,9 @@ from typing import Optional
 import numpy as np
 
 # row sums of the device and the oracle agree within this many ulps of the
-# round's largest row sum (stated bound; the sweeps record the measured ones)
-DEV_ULPS = 64
+# round's largest row sum (stated bound; the sweeps record the measured
+# ones), plus one ulp per round for the matrix-free form
+DEV_ULPS = 16
 
 
 def max_dsum(s: np.ndarray, cyclic: bool):
@@ -61,7 +67,7 @@ def first_stop(sums: np.ndarray, eps, cyclic: bool) -> Optional[int]:
 
 
 def compare(gpu_sums: np.ndarray, orc_sums: np.ndarray, eps, cyclic: bool,
-            max_itr: int) -> dict:
+            max_itr: int, matrix_free: bool = False) -> dict:
     """Check two traces (shape (rounds, n), one row per evaluated round) and
     return a summary:
       consistent  both traces stop where their solves stopped
@@ -69,6 +75,8 @@ def compare(gpu_sums: np.ndarray, orc_sums: np.ndarray, eps, cyclic: bool,
                   first round whose decisions differ
       same_stop   the solves stopped in the same round (=> equal counts)
       dev_ulps    per compared round, max |s_gpu - s_oracle| / ulp(max s)
+      dev_excess  rounds whose deviation exceeds the bound (DEV_ULPS, plus
+                  the round index for the matrix-free form)
     A solve that ran out of rounds evaluated max_itr rounds and stopped in
     none of them."""
     out = {"rounds_gpu": int(gpu_sums.shape[0]), "rounds_oracle": int(orc_sums.shape[0])}
@@ -92,6 +100,8 @@ def compare(gpu_sums: np.ndarray, orc_sums: np.ndarray, eps, cyclic: bool,
             straddle = {"round": k, "dmax_gpu": dg, "dmax_oracle": do,
                         "margin": abs(do - float(o.dtype.type(eps))), "dev": dev}
     out["dev_ulps"] = [round(x, 2) for x in dev_ulps]
+    out["dev_excess"] = [k for k, x in enumerate(dev_ulps)
+                         if x > DEV_ULPS + (k if matrix_free else 0)]
     out["max_dev_ulps"] = round(max(dev_ulps), 2) if dev_ulps else 0.0
     out["straddle"] = straddle
     out["same_stop"] = gpu_sums.shape[0] == orc_sums.shape[0]
@@ -102,7 +112,7 @@ def assert_stop_parity(cmp: dict, tag=None) -> bool:
     """Assert what ``compare`` found is legitimate; returns True when the
     counts must agree (no straddle), False for a reported straddle."""
     assert cmp["consistent"], ("trace does not stop where its solve stopped", tag, cmp)
-    assert cmp["max_dev_ulps"] <= DEV_ULPS, ("row sums deviate", tag, cmp)
+    assert not cmp["dev_excess"], ("row sums deviate", tag, cmp)
     st = cmp["straddle"]
     if st is None:
         assert cmp["same_stop"], ("no straddling round, yet different stop rounds", tag, cmp)

@@ -1012,7 +1012,7 @@ def test_fuzz_vs_oracle(eigen, orc):
         ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=200, trace=True)
         tag = (case, n, dt.__name__, sem, mf, batch, eps, kind)
         cmp = sp.compare(eigen.last_round_sums(), ref.row_sums, dt(eps),
-                         sem == _lib.ST_SEM_SYCL, 200)
+                         sem == _lib.ST_SEM_SYCL, 200, matrix_free=mf)
         if not sp.assert_stop_parity(cmp, tag):
             straddles.append((tag, cmp["straddle"]))
             continue
@@ -1060,7 +1060,8 @@ def test_trace_sums_round_trip(eigen, solver, orc):
         assert lam == base[0] and itr == base[3] and np.array_equal(v, base[1])
         assert sums.shape == (st["rounds"], n) and sums.dtype == dt
         ref = orc.similarity_transform(mat, orc.SEM_SYCL, trace=True)
-        cmp = sp.compare(sums, ref.row_sums, dt(1e-3), True, orc.MAX_ITR)
+        cmp = sp.compare(sums, ref.row_sums, dt(1e-3), True, orc.MAX_ITR,
+                         matrix_free=kw.get("matrix_free", False))
         assert sp.assert_stop_parity(cmp, n) and itr == ref.iter_count
         t = torch.from_numpy(mat).to(DEV)
         lam_d, v_d, it_d, st_d = solver.solve(t, trace_sums=True, **kw)

@@ -221,3 +221,44 @@ def test_oracle_under_sanitizers(tmp_path):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr[-3000:]
     assert "clean" in out.stdout
+
+
+def test_stop_parity_rule():
+    """tests/stop_parity.py on synthetic traces (fp32, cyclic, eps = 1.0):
+    identical traces agree; a round whose max |ds| straddles eps by less
+    than the row sums' deviation excuses different counts; a deviation past
+    DEV_ULPS (plus the round index for the matrix-free form) fails; a trace
+    that does not stop where its solve stopped fails."""
+    import stop_parity as sp
+    f = np.float32
+    orc = np.array([[1, 4, 1, 4], [2, 2.5, 2, 2.5]], f)          # stops in round 1
+    assert sp.first_stop(orc, f(1.0), True) == 1
+    c = sp.compare(orc, orc.copy(), f(1.0), True, 100)
+    assert sp.assert_stop_parity(c) and c["straddle"] is None and c["max_dev_ulps"] == 0
+    # the device's round-1 sums 3 ulps apart put max |ds| just past eps
+    u = np.spacing(f(2.5))
+    gpu = np.array([[1, 4, 1, 4],
+                    [2, 2.5, 2, 2.5],
+                    [2, 2.25, 2, 2.25]], f)
+    gpu[1, 1] = gpu[1, 3] = f(3.0) + u        # max |ds| 1 + u: no stop
+    orc2 = orc.copy()
+    orc2[1, 1] = orc2[1, 3] = f(3.0) - u      # max |ds| 1 - u: stops
+    gpu[1, 1] = gpu[1, 3] = f(3.0) + 2 * u
+    c = sp.compare(gpu, orc2, f(1.0), True, 100)
+    assert c["straddle"] is not None and c["straddle"]["round"] == 1
+    assert sp.assert_stop_parity(c) is False                   # listed, not failed
+    # a deviation of 1000 ulps is not rounding
+    bad = orc2.copy()
+    bad[0, 1] += 1000 * np.spacing(f(4.0))
+    with pytest.raises(AssertionError, match="row sums deviate"):
+        sp.assert_stop_parity(sp.compare(bad, orc2, f(1.0), True, 100))
+    # ... but the matrix-free form may drift one ulp per round
+    drift = np.repeat(orc2[:1], 40, axis=0)
+    drift[:, 0] = f(1.0)
+    mf = drift.copy()
+    mf[39, 1] += 40 * np.spacing(f(4.0))
+    assert sp.compare(mf, drift, f(1.0), True, 40)["dev_excess"] == [39]
+    assert sp.compare(mf, drift, f(1.0), True, 40, matrix_free=True)["dev_excess"] == []
+    # a trace that passes the stop test before its last round is inconsistent
+    with pytest.raises(AssertionError, match="does not stop"):
+        sp.assert_stop_parity(sp.compare(np.vstack([orc, orc[1:]]), orc, f(1.0), True, 100))

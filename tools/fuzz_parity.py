@@ -46,6 +46,7 @@ def main():
     flat = [4352, 4353, 4480, 5000, 5121, 6144]           # >= 144 MiB fp64: the flat round
     worst = {"f64": {"lam": 0.0, "v": 0.0}, "f32": {"lam": 0.0, "v": 0.0}}
     out = {"seed": a.seed, "cases": [], "straddles": [], "dev_ulps_max": {"f64": 0.0, "f32": 0.0},
+           "dev_ulps_max_transform": {"f64": 0.0, "f32": 0.0},
            "rule": "tests/stop_parity.py: traced row sums on both sides; a count may differ "
                    "only in a round whose max|ds| straddles eps between the two solves"}
     solver = dev.DeviceSolver("cuda:0")
@@ -81,8 +82,12 @@ def main():
             ref = orc.similarity_transform(mat, sem, eps=dt(eps), max_itr=max_itr,
                                            nthreads=16, trace=True)
             key = "f64" if dt == np.float64 else "f32"
-            cmp = sp.compare(sums, ref.row_sums, dt(eps), sem == 0, max_itr)
+            cmp = sp.compare(sums, ref.row_sums, dt(eps), sem == 0, max_itr,
+                             matrix_free=form == "mfree")
             out["dev_ulps_max"][key] = max(out["dev_ulps_max"][key], cmp["max_dev_ulps"])
+            if form != "mfree":
+                out["dev_ulps_max_transform"][key] = max(out["dev_ulps_max_transform"][key],
+                                                         cmp["max_dev_ulps"])
             try:
                 must_match = sp.assert_stop_parity(cmp, case)
                 trace_ok = True
@@ -115,6 +120,8 @@ def main():
     out["n_cases"] = len(out["cases"])
     out["n_ok"] = sum(c["ok"] for c in out["cases"])
     out["seconds"] = round(time.time() - t0, 1)
+    out["straddles_by_eps"] = {str(e): sum(1 for c in out["straddles"] if c["eps"] == e)
+                               for e in (1e-3, 1e-6, 1e-2)}
     # the fp32 random cases the reference's own shape covers (N >= 200,
     # wrapper/python/test.py), per eps
     out["f32_random_n200_checked"] = {

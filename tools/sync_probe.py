@@ -6,7 +6,8 @@ over 20 rounds and K = 200 (the builder's old default) over 200.  For the
 configs[1] round (k_flat + k_parts, Hilbert 8192^2 fp64) this prints, per K:
 host ms per round, HIP-event ms per round and the difference times K (the
 fixed part), plus the cost of an idle synchronize and of an event round
-trip.  Run as is and with HSA_ENABLE_INTERRUPT=0 (the runtime then polls
+trip, and K = 20 once more with an amdgpu sysfs clock read right before t0
+(`20+clocks`).  Run as is and with HSA_ENABLE_INTERRUPT=0 (the runtime then polls
 completion signals instead of sleeping on an interrupt).
 
     python3 tools/sync_probe.py [--json OUT]
@@ -48,8 +49,11 @@ def main():
     out["event_roundtrip_us"] = round(sorted(t)[len(t) // 2] * 1e6, 2)
     sh = ShardedSimilarityTransform(8192, torch.float64)
     sh.load("hilbert")
+    import bench
     res = {}
-    for k in (1, 5, 20, 200):
+    for k in (1, 5, 20, 200, "20+clocks"):
+        clocks = isinstance(k, str)
+        kk = 20 if clocks else k
         rows = []
         for _ in range(a.reps):
             sh.load("hilbert")
@@ -57,14 +61,16 @@ def main():
             sh.rounds(5, 0.0, 2 ** 31)
             ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
             torch.cuda.synchronize()
+            if clocks:   # an amdgpu sysfs clock read right before t0 (round 6's first bench)
+                bench.gpu_clocks(torch, 0)
             t0 = time.perf_counter()
             ev[0].record()
-            sh.rounds(k, 0.0, 2 ** 31)
+            sh.rounds(kk, 0.0, 2 ** 31)
             ev[1].record()
             torch.cuda.synchronize()
             el = time.perf_counter() - t0
             evm = ev[0].elapsed_time(ev[1])
-            rows.append((el * 1e3 / k, evm / k, (el * 1e3 - evm) * 1e3))
+            rows.append((el * 1e3 / kk, evm / kk, (el * 1e3 - evm) * 1e3))
         rows.sort(key=lambda r: r[0])
         med = rows[len(rows) // 2]
         res[str(k)] = {"host_ms_per_round": round(med[0], 5), "event_ms_per_round": round(med[1], 5),
