@@ -26,6 +26,11 @@ smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -
 fuzz) run fuzz 900 python3 -u tools/fuzz_parity.py --cases ${FUZZ_CASES:-300} --seed ${FUZZ_SEED:-20261201} --json $O/r06_fuzz_parity.json; tail -3 $O/fuzz.log; grep -c STRADDLE $O/fuzz.log ;;
 bench) run bench 900 python3 bench.py --steps 20 --warmup 5; tail -c 1500 $O/bench.log ;;
 benchquick) run benchquick 600 python3 bench.py --steps 20 --warmup 5 --no-cpu --no-north-star --no-headline; tail -c 2500 $O/benchquick.log ;;
+profdefault)
+  # the default bench line under a kernel trace (the driver's command)
+  D=$O/profdefault; mkdir -p $D
+  run prof_default 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --steps 20 --warmup 5
+  head -8 $D/run_kernel_stats.csv | cut -c1-200 ;;
 prof)
   D=$O/prof; mkdir -p $D
   run prof_bench 900 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu --no-north-star --no-headline
