@@ -124,6 +124,10 @@ class HipShardOps:
             self.dev.fused_round(mat, s_cur, s_next, v, row0=row0, eps=eps, k=k,
                                  max_itr=max_itr, semantics=semantics, state=state)
 
+    def current_stream_id(self) -> int:
+        """The launch stream round_call captures (its cache key in rounds())."""
+        return self.torch.cuda.current_stream(self.device).cuda_stream
+
     def round_call(self, mat, s_cur, s_next, v, v_next, row0, eps, max_itr, semantics,
                    state, matrix_free=False):
         """The launch of round() (or mfree_round()) for these buffers with
@@ -580,7 +584,7 @@ class ShardedSimilarityTransform:
             for _ in range(count):
                 self.round(eps, max_itr)
             return
-        key = (eps, max_itr, self.mat.data_ptr(), self.torch.cuda.current_stream().cuda_stream)
+        key = (eps, max_itr, self.mat.data_ptr(), self.ops.current_stream_id())
         if getattr(self, "_calls_key", None) != key:
             calls = []
             for par in (0, 1):

@@ -692,3 +692,89 @@ def test_make_comm_agreed_does_not_all_reduce_past_a_missing_rank(tmp_path):
     all-reduce (which would wait for the absent rank forever)."""
     mp.spawn(_agree_missing_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     assert [open(tmp_path / f"m{r}").read() for r in range(2)] == ["raised", "raised"]
+
+
+# ---------------------------------------------------------------------------
+# ShardedSimilarityTransform.rounds(): the bench's pre-resolved launch path,
+# with a stand-in library communicator, against round() at world 2 and 3
+# ---------------------------------------------------------------------------
+class CpuFastOps(CpuShardOps):
+    """CpuShardOps plus the round_call contract of HipShardOps (fn(*pre, k,
+    *post) launches round k), as Python callables."""
+
+    def current_stream_id(self):
+        return 0
+
+    def round_call(self, mat, s_cur, s_next, v, v_next, row0, eps, max_itr, semantics, st,
+                   matrix_free=False):
+        if matrix_free:
+            def fn(m, sc, sn, vp, vc, r0, e, k, mi, sem, state, _stream):
+                self.mfree_round(m, sc, sn, vp, vc, r0, e, k, mi, sem, state)
+                return 0
+            return fn, (mat, s_cur, s_next, v, v_next, row0, eps), (max_itr, semantics, st, 0)
+
+        def fn(m, sc, sn, vv, r0, e, k, mi, sem, state, _stream):
+            self.round(m, sc, sn, vv, r0, e, k, mi, sem, state)
+            return 0
+        return fn, (mat, s_cur, s_next, v, row0, eps), (max_itr, semantics, st, 0)
+
+
+class _GlooComm:
+    """Stand-in for RcclComm: allgather / allgather_call over the gloo group."""
+
+    def allgather(self, out, inp):
+        fn, args = self.allgather_call(out, inp)
+        fn(*args)
+
+    def allgather_call(self, out, inp):
+        from eigen_value_amd.sharded import _allgather
+
+        def fn(o, i):
+            _allgather(o, i)
+            return 0
+        return fn, (out, inp)
+
+    def close(self):
+        pass
+
+
+def _fast_worker(rank, world, port, n, mf, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = []
+        for fast in (False, True):
+            sh = ShardedSimilarityTransform(n, torch.float64, ops=CpuFastOps(), matrix_free=mf,
+                                            comm="torch")
+            sh.rccl = _GlooComm() if fast else None
+            sh.load("random", seed=5)
+            sh.start()
+            for eps, k in ((0.0, 3), (1e-3, 12)):      # fixed rounds, then to a stop
+                if fast:
+                    sh.rounds(k, eps, 50)
+                else:
+                    for _ in range(k):
+                        sh.round(eps, 50)
+            st = sh.ops.read_state(sh.state)
+            res.append((st["eigen_val"], st["iters"], st["end"], sh.k, sh.cur,
+                        [x.clone() for x in sh.s], sh.mat.clone()))
+        (a, b) = res
+        same = a[:5] == b[:5] and all(torch.equal(x, y) for x, y in zip(a[5], b[5])) \
+            and torch.equal(a[6], b[6])
+        np.save(os.path.join(outdir, f"fast{rank}.npy"), np.array([same, a[0], a[1]]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n,mf", [(2, 301, False), (3, 300, True), (2, 64, False)])
+def test_rounds_fast_path_matches_round(tmp_path, world, n, mf):
+    """rounds() through pre-resolved launches and a communicator's
+    allgather_call (the path the 8-GPU bench takes with the library RCCL
+    communicator) leaves every rank's row sums, matrix, state, k and ping-pong
+    parity exactly as round() does, for the transform and the matrix-free
+    form, through a stop and the gated rounds after it."""
+    mp.spawn(_fast_worker, args=(world, _free_port(), n, mf, str(tmp_path)), nprocs=world,
+             join=True)
+    for r in range(world):
+        same, lam, it = np.load(tmp_path / f"fast{r}.npy")
+        assert bool(same), r

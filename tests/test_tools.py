@@ -131,7 +131,7 @@ def test_citation_checker_expands_ellipsis_names():
     assert cc.expand_ellipsis("r03_defer_cycle_x.json", "_launches.csv") == \
         "r03_defer_cycle_x_launches.csv"
     pats = cc.cited_patterns()
-    assert "r01_sweep_dir_policy_table.txt" in pats
+    assert any(p.startswith("r06_") for p in pats)
     assert cc.uncited() == []
 
 
