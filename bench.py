@@ -443,9 +443,8 @@ def timed_rounds(sh, steps, warmup, torch, dist, world, clocks_key=None):
     the timed region runs without events, and a separate pass after it
     brackets each launch with its own pair for the kernel average."""
     cool_down(torch)
-    # the clock levels are read before the warm-up rounds, not at t0: an
-    # amdgpu sysfs clock read asks the SMU, and the launches right after it
-    # start late (tools/sync_probe.py --clocks)
+    # the clock levels are read before the warm-up rounds, not at t0, so the
+    # amdgpu sysfs read (an SMU query) stays out of the timed region
     if clocks_key:
         CLOCKS[clocks_key + "_before"] = gpu_clocks(torch, torch.cuda.current_device())
     sh.start()

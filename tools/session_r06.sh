@@ -45,6 +45,9 @@ sync)
   # the host clock's fixed start / stop latency
   run sync_default 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_default.json; tail -6 $O/sync_default.log
   HSA_ENABLE_INTERRUPT=0 run sync_polling 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_polling.json; tail -6 $O/sync_polling.log ;;
+prefix)
+  # the headline pass fresh and after each step bench.py runs before it
+  run prefix 300 python3 -u tools/prefix_probe.py --json $O/r06_prefix_probe.json; cat $O/prefix.log | tail -12 ;;
 pmc)
   # kernel trace + FETCH_SIZE / WRITE_SIZE passes of the bench's own legs
   # for the headline workload and the north star (fp64, fp32), one process
