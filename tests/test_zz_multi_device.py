@@ -95,15 +95,20 @@ def test_native_multi_gpu_all_devices(orc, ngpus):
     _free()
 
 
-def _comm_worker(rank, world, port, outdir, rehearsal=False):
+def _comm_worker(rank, world, port, outdir, rehearsal=False, interface=False):
     """One rank: the library communicator's in-slot all-gather, then the
     sharded solve of a k_round and a flat (deferred) block.  rehearsal:
     every rank on cuda:0 over gloo with the torch all-gather, the same
-    body otherwise."""
+    body otherwise.  interface: the rendezvous advertises the library's
+    interface choice instead of the loopback address (an empty ST_COMM_ADDR
+    makes RcclComm pass no address, and the library ignores the empty
+    value: NCCL_SOCKET_IFNAME's or the first up non-loopback interface)."""
     import torch.distributed as dist
     from eigen_value_amd import _lib
     from eigen_value_amd.sharded import RcclComm, ShardedSimilarityTransform, _allgather
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if interface:
+        os.environ["ST_COMM_ADDR"] = ""
     dev_index = 0 if rehearsal else rank
     torch.cuda.set_device(dev_index)
     if rehearsal:
@@ -180,6 +185,18 @@ def test_library_comm_all_devices(tmp_path, orc, world):
     the oracle."""
     import torch.multiprocessing as mp
     mp.spawn(_comm_worker, args=(world, _port(), str(tmp_path)), nprocs=world, join=True)
+    _check_comm_run(tmp_path, orc, world, distinct=True)
+
+
+@pytest.mark.parametrize("world", _multi_counts()[:1])
+def test_library_comm_interface_choice(tmp_path, orc, world):
+    """test_library_comm_all_devices at the smallest P with the rendezvous
+    on the library's own interface choice (st_comm_unique_id_addr(NULL)) -
+    the multi-host default - instead of the loopback address sharded.py
+    uses when every rank is on this host."""
+    import torch.multiprocessing as mp
+    mp.spawn(_comm_worker, args=(world, _port(), str(tmp_path), False, True), nprocs=world,
+             join=True)
     _check_comm_run(tmp_path, orc, world, distinct=True)
 
 
