@@ -585,7 +585,10 @@ class ShardedSimilarityTransform:
                 self.round(eps, max_itr)
             return
         key = (eps, max_itr, self.mat.data_ptr(), self.ops.current_stream_id())
-        if getattr(self, "_calls_key", None) != key:
+        # the resolved launches hold the ops' flat scratch by address: rebuild
+        # them whenever that scratch was replaced (another shape used the ops)
+        cached = getattr(self, "_calls_key", None)
+        if cached is None or cached[0] != key or cached[1] is not getattr(self.ops, "_part", None):
             calls = []
             for par in (0, 1):
                 if self.matrix_free:
@@ -602,7 +605,7 @@ class ShardedSimilarityTransform:
                     g = self.rccl.allgather_call(self.s[par ^ 1],
                                                  self.s[par ^ 1][p.rank * p.chunk:(p.rank + 1) * p.chunk])
                 calls.append((c, g))
-            self._calls, self._calls_key = calls, key
+            self._calls, self._calls_key = calls, (key, getattr(self.ops, "_part", None))
         L = _lib.load()
         for _ in range(count):
             (fn, pre, post), g = self._calls[self.k & 1]
