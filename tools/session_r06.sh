@@ -45,6 +45,17 @@ sync)
   # the host clock's fixed start / stop latency
   run sync_default 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_default.json; tail -6 $O/sync_default.log
   HSA_ENABLE_INTERRUPT=0 run sync_polling 300 python3 tools/sync_probe.py --json $O/r06_sync_probe_polling.json; tail -6 $O/sync_polling.log ;;
+tables)
+  # the reference's own benchmark tables (README.md whole-solve Hilbert,
+  # benchmarks/similarity_transform.md per kernel) through the C-ABI, and
+  # the flat walk's own memory ceiling (no arithmetic)
+  run tables_hilbert 300 bash -c './tools/bench_hilbert f32 && ./tools/bench_hilbert f64' && \
+  run tables_kernels 300 ./tools/bench_kernels && \
+  run tables_mall 300 ./tools/mall_stream 8192x8192 32768x32768; tail -40 $O/tables_*.log ;;
+everyab)
+  # the every-round flat launch of configs[1] under workgroup caps / tiles
+  # (tuning build; interleaved passes of 20 rounds)
+  EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run everyab 400 python3 -u tools/defer_profile.py --n 8192 --kind hilbert --every-ab "${EVERY_AB:-0;0:0:3;0:0:4;0:0:6;0:4;0:16}" --steps 20 --passes 9 --ab-json $O/r06_every_ab.json; tail -8 $O/everyab.log ;;
 prefix)
   # the headline pass fresh and after each step bench.py runs before it
   run prefix 300 python3 -u tools/prefix_probe.py --json $O/r06_prefix_probe.json; cat $O/prefix.log | tail -12 ;;
