@@ -107,6 +107,43 @@ def test_rowsum_vs_oracle(orc, dt, nrows, ncols):
 
 
 @pytest.mark.parametrize("dt", [np.float64, np.float32])
+@pytest.mark.parametrize("nrows,ncols", [(1, 1), (5, 3), (37, 1001), (2051, 256), (333, 8200),
+                                         (1031, 4099), (64, 12288)])
+def test_rowsum_flat_vs_oracle(orc, dt, nrows, ncols):
+    """K0 in the flat form (st_rowsum_flat: k_flat_sum + k_parts), the solve
+    loops' initial row sums wherever the flat round pays, at any shape -
+    ragged pieces, odd row counts, columns no multiple of the vector width
+    (similarity_transform.cpp:40, the first sum_across_rows): against the
+    oracle to rounding, and bit for bit the flat round's own sums of the
+    same matrix (a round with unit scales leaves A unchanged: x·((1/1)·1) =
+    x), and partition-independent: any row block's sums equal the same rows'
+    sums in the whole block."""
+    a = orc.random_matrix(ncols, 11, dt, nrows=nrows)
+    ta = torch.from_numpy(a).to(DEV)
+    part = dev.flat_scratch(nrows, ncols, TD[dt], DEV)
+    got = torch.empty(nrows, dtype=TD[dt], device=DEV)
+    dev.rowsum_flat(ta, got, part)
+    got = to_np(got)
+    ref = orc.rowsum(a)
+    tol = 1e-13 if dt == np.float64 else 2e-6
+    assert np.max(np.abs(got - ref) / np.abs(ref)) <= tol
+    # the flat round's sums, unit scales (a row block inside the s vector)
+    if nrows <= ncols:
+        ones = torch.ones(ncols, dtype=TD[dt], device=DEV)
+        s_next = torch.empty(nrows, dtype=TD[dt], device=DEV)
+        v = torch.ones(ncols, dtype=TD[dt], device=DEV)
+        dev.flat_round(ta, ones, s_next, part, v, dev.new_state(DEV), eps=0.0, k=0)
+        assert np.array_equal(to_np(ta), a)
+        assert np.array_equal(to_np(s_next), got)
+    # a row block of the same columns
+    r0, r1 = nrows // 3, nrows // 3 + max(1, nrows // 2)
+    sub = torch.from_numpy(np.ascontiguousarray(a[r0:r1])).to(DEV)
+    got_sub = torch.empty(r1 - r0, dtype=TD[dt], device=DEV)
+    dev.rowsum_flat(sub, got_sub, dev.flat_scratch(r1 - r0, ncols, TD[dt], DEV))
+    assert np.array_equal(to_np(got_sub), got[r0:r1])
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.float32])
 @pytest.mark.parametrize("sem", [_lib.ST_SEM_SYCL, _lib.ST_SEM_MAINPY])
 @pytest.mark.parametrize("nrows,ncols,row0", [(3, 3, 0), (64, 257, 100), (2050, 4096, 1000), (4099, 4100, 1)])
 def test_fused_step_vs_oracle(orc, dt, sem, nrows, ncols, row0):
