@@ -1296,21 +1296,28 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
 // piece, 0 = row-major), without its scaling.  Replaces the grid-stride
 // k_fused launch, which streamed the same bytes at 0.77 / 0.83 of 8 TB/s
 // (8192^2 / 32768^2 fp64) where the flat read-only round ran 0.88 / 0.90.
+// rev: walk the pieces from the end of the block (an odd round's order,
+// flat_reverse<2>): on a cacheable block just written front to back (a
+// generator, the drop-in's host copy) the walk starts on what the memory-side
+// cache still holds, and leaves the block's start there for round 0.
 template <typename T, int W, bool NT, int R, int U, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_flat_sum(const T* __restrict__ a, T* __restrict__ part, uint32_t nrows,
-           uint32_t ncols, uint32_t ppr, uint32_t pt, uint32_t gx2)
+           uint32_t ncols, uint32_t ppr, uint32_t pt, uint32_t gx2, uint32_t rev)
 {
   using V = typename vec<T, W>::type;
   constexpr int NW = BLK / 64;
   __shared__ T red[NW][R];
   const uint32_t ng = (nrows + R - 1) / R;
-  uint32_t b = blockIdx.x;
+  uint32_t b = blockIdx.x, nb = gridDim.x;
   if (gx2 != 0) { // a 2-D grid (k_flat's gx2): fold blockIdx.y back in
     b += blockIdx.y * gx2;
-    if (b >= ng * ppr)
+    nb = ng * ppr;
+    if (b >= nb)
       return;
   }
+  if (rev)
+    b = flat_reverse<2>(b, nb);
   uint32_t rg, p;
   if (pt != 0) { // pt row groups of one piece back to back (k_flat's order)
     const uint32_t tile = b / (pt * ppr), t = b - tile * (pt * ppr);

@@ -1374,6 +1374,11 @@ launch_rowsum(const T* a, T* s, uint32_t nrows, uint32_t ncols,
   return check_launch("rowsum");
 }
 
+// K0's walk order (k_flat_sum's rev): -1 = reversed where the loads go
+// through the caches (the block is memory-side-cacheable), 0 = front to back
+// (the default), 1 = reversed; st_set_k0_reverse (tuning build)
+std::atomic<int> g_k0_rev{ 0 };
+
 // K0 in the flat form (k_flat_sum + k_parts) for blocks where the flat round
 // pays: the pieces (kFlatU), rows per workgroup and walk order (defer_rows /
 // defer_tile), workgroups-per-CU cap and load policy (g_defer_flip bit 0) of
@@ -1392,12 +1397,14 @@ launch_rowsum_flat_cfg(const T* a, T* s, T* part, uint32_t nrows, uint32_t ncols
   const uint32_t lds = defer_lds<T, NT>(0);
   const FlatGrid fg = flat_grid((nrows + R - 1) / R * ppr);
   const bool flip = W > 1 && (defer_flip<T>(nrows, ncols) & 1u) != 0;
+  const int rv = g_k0_rev.load(std::memory_order_relaxed);
+  const uint32_t rev = rv < 0 ? (NT == flip ? 1u : 0u) : (uint32_t)rv;
   if (NT != flip)
     hipLaunchKernelGGL((dev::k_flat_sum<T, W, true, R, U>), fg.grid, dim3(kBlock), lds,
-                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2);
+                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2, rev);
   else
     hipLaunchKernelGGL((dev::k_flat_sum<T, W, false, R, U>), fg.grid, dim3(kBlock), lds,
-                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2);
+                       stream, a, part, nrows, ncols, ppr, pt, fg.gx2, rev);
   launch_parts<T>(part, s, nrows, ppr, 0u, nullptr, nullptr, nullptr, 0u, nullptr, stream);
 }
 
@@ -1645,7 +1652,8 @@ policy_flat(uint32_t nrows, uint32_t ncols, int form, uint32_t np,
     o->cap = g_defer_caps[sizeof(T) == 8][NT][0].load(std::memory_order_relaxed);
     o->load_nt = NT != ((defer_flip<T>(nrows, ncols) & 1u) != 0);
     o->store_nt = -1;
-    o->alt = 0;
+    const int rv = g_k0_rev.load(std::memory_order_relaxed);
+    o->alt = rv < 0 ? (o->load_nt ? 0 : 1) : rv; // launch_rowsum_flat_cfg's rev
     return 0;
   }
   const bool store = form == ST_FORM_DEFER_STORE;
@@ -2067,6 +2075,12 @@ st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype)
   }
   return (int)st::every_cache_class(
     st::block_bytes(nrows, ncols, dtype == 1 ? 8 : 4));
+}
+
+int
+st_set_k0_reverse(int mode)
+{
+  return st::g_k0_rev.exchange(mode < 0 ? -1 : (mode ? 1 : 0), std::memory_order_relaxed);
 }
 
 unsigned int

@@ -33,6 +33,13 @@ extern "C" {
  * it. */
 unsigned int st_set_flat_grid_limit(unsigned int max_x);
 
+/* K0's walk order in the flat form (st_rowsum_flat and the solve loops'
+ * initial row sums): -1 = pieces walked from the end of the block where its
+ * loads go through the caches, 0 = front to back (the library's default),
+ * 1 = from the end.  Results do not depend on it (each piece's partial sum
+ * and k_parts' order are fixed).  Returns the previous mode. */
+int st_set_k0_reverse(int mode);
+
 /* Workgroups per CU of the deferred flat round's launches (dtype 0 = f32,
  * 1 = f64; nontemporal = the launch form of blocks >= 2 GiB, else the cached
  * one; slot 0..4 = a read-only round with that many pending rounds, 6 =

@@ -56,6 +56,9 @@ everyab)
   # the every-round flat launch of configs[1] under workgroup caps / tiles
   # (tuning build; interleaved passes of 20 rounds)
   EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run everyab 400 python3 -u tools/defer_profile.py --n 8192 --kind hilbert --every-ab "${EVERY_AB:-0;0:0:3;0:0:4;0:0:6;0:4;0:16}" --steps 20 --passes 9 --ab-json $O/r06_every_ab.json; tail -8 $O/everyab.log ;;
+k0order)
+  # K0 walked front to back vs from the end on cacheable blocks (tuning build)
+  EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run k0order 400 python3 -u tools/k0_order_probe.py --json $O/r06_k0_order.json; tail -8 $O/k0order.log ;;
 prefix)
   # the headline pass fresh and after each step bench.py runs before it
   run prefix 300 python3 -u tools/prefix_probe.py --json $O/r06_prefix_probe.json; cat $O/prefix.log | tail -12 ;;
