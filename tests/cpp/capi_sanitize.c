@@ -128,6 +128,10 @@ main(void)
   CHECK(old >= 0 && st_set_defer_caps(1, 1, 6, (unsigned)old) == 5);
   CHECK(st_set_every_cache(9, 0) < 0);
   CHECK(st_set_mfree_shape(9) < 0);
+  {
+    const int k0 = st_set_k0_reverse(1);
+    CHECK(k0 >= -1 && k0 <= 1 && st_set_k0_reverse(k0) == 1);
+  }
   CHECK(st_defer_ntload_class(8192, 8192, 7) < 0);
   CHECK(st_every_cache_class(8192, 8192, 1) == 1);
   CHECK(st_round_flat_pays(8192, 8192, 1) == 1 && st_defer_rounds(8192, 8192, 1) == 6);
