@@ -36,6 +36,18 @@ $(LIB_TUNING): $(TUNING_OBJ)
 	@mkdir -p eigen_value_amd/lib
 	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(TUNING_OBJ) -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
+# an A/B probe build of the launch-shape / kernel-code switches
+# (st_kernels.hip, st_device.h): make probe PROBE="-DST_FLAT_ALT=0"; run a
+# tool with EIGEN_VALUE_LIB pointing at the result (st_version names the
+# switches); never a product build
+PROBE_LIB := eigen_value_amd/lib/variants/libsimilarity_transform_probe.so
+probe: $(SRC) $(HDRS)
+	@mkdir -p build/probe eigen_value_amd/lib/variants
+	for f in $(SRC); do $(HIPCC) $(HIPFLAGS) -DST_TUNING_ABI=1 -DST_PROBES=1 $(PROBE) \
+	  -c $$f -o build/probe/$$(basename $$f .hip).o || exit 1; done
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $(PROBE_LIB) build/probe/*.o \
+	  -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -43,4 +55,4 @@ clean:
 	rm -rf build eigen_value_amd/lib
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean probe

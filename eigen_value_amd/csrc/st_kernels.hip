@@ -28,10 +28,10 @@
 
 // A/B probe switches of the launch shapes (st_device.h has those of the
 // kernel code: ST_DPP_NOINIT, ST_ROW_VLOAD, ST_FLAT_UNMASKED,
-// ST_DEFER_STORE_NT).  Probe builds of the library
-// (tools/defer_shape_probe.sh) pass -DST_PROBES=1 with other values; a
-// library build with any other value fails here, and st_version() names the
-// switches a probe build was made with.
+// ST_DEFER_STORE_NT).  A probe build of the library (`make probe
+// PROBE="-DST_FLAT_ALT=0"`, eigen_value_amd/lib/variants/) passes
+// -DST_PROBES=1 with other values; a library build with any other value
+// fails here, and st_version() names the switches a probe build was made with.
 #ifndef ST_EVERY_CACHED_R1 // 0 = round 2's 2 rows, row-major
 #define ST_EVERY_CACHED_R1 1
 #endif
