@@ -15,6 +15,13 @@ row-sum deviation in ulps is recorded.  Test infrastructure: the oracle is
 the checker.
 
     python3 tools/fuzz_parity.py --cases 300 --json OUT.json
+    python3 tools/fuzz_parity.py --profile wrapper --cases 200 --json OUT.json
+
+`--profile wrapper`: only the reference's own wrapper-test shape
+(wrapper/python/test.py:3-18) - fp32 random matrices through the drop-in
+max_eigen_value at its EPS = 1e-3f and MAX_ITR = 1000, SYCL semantics, the
+default (deferred-write) form - at N log-uniform over 200 .. 8192, so that
+the fp32 flat path (N >= 6145) is in it too.
 """
 import argparse
 import json
@@ -32,6 +39,7 @@ def main():
     p.add_argument("--cases", type=int, default=300)
     p.add_argument("--seed", type=int, default=20261017)
     p.add_argument("--json", default=None)
+    p.add_argument("--profile", choices=["mixed", "wrapper"], default="mixed")
     a = p.parse_args()
     import numpy as np
     import torch
@@ -45,7 +53,7 @@ def main():
              1024, 1025, 2047, 2049, 2051, 3001]
     flat = [4352, 4353, 4480, 5000, 5121, 6144]           # >= 144 MiB fp64: the flat round
     worst = {"f64": {"lam": 0.0, "v": 0.0}, "f32": {"lam": 0.0, "v": 0.0}}
-    out = {"seed": a.seed, "cases": [], "straddles": [], "dev_ulps_max": {"f64": 0.0, "f32": 0.0},
+    out = {"seed": a.seed, "profile": a.profile, "cases": [], "straddles": [], "dev_ulps_max": {"f64": 0.0, "f32": 0.0},
            "dev_ulps_max_transform": {"f64": 0.0, "f32": 0.0},
            "rule": "tests/stop_parity.py: traced row sums on both sides; a count may differ "
                    "only in a round whose max|ds| straddles eps between the two solves"}
@@ -53,16 +61,21 @@ def main():
     t0 = time.time()
     with EigenValue() as ev:
         for case in range(a.cases):
-            big = rng.random() < 0.25
-            n = int(rng.choice(flat if big else small))
-            dt = np.float64 if (big or rng.random() < 0.6) else np.float32
-            sem = int(rng.integers(0, 2))
-            form = str(rng.choice(["deferred", "every", "mfree"]))
-            batch = int(rng.choice([0, 1, 2, 5, 8]))
-            eps = float(rng.choice([1e-3, 1e-6, 1e-2]))
-            kind = "hilbert" if rng.random() < 0.5 else "random"
-            path = "device" if rng.random() < 0.5 else "dropin"
-            max_itr = 60 if big else 200
+            if a.profile == "wrapper":
+                n = int(round(np.exp(rng.uniform(np.log(200), np.log(8192)))))
+                dt, sem, form, batch, eps = np.float32, 0, "deferred", 0, 1e-3
+                kind, path, max_itr = "random", "dropin", orc.MAX_ITR
+            else:
+                big = rng.random() < 0.25
+                n = int(rng.choice(flat if big else small))
+                dt = np.float64 if (big or rng.random() < 0.6) else np.float32
+                sem = int(rng.integers(0, 2))
+                form = str(rng.choice(["deferred", "every", "mfree"]))
+                batch = int(rng.choice([0, 1, 2, 5, 8]))
+                eps = float(rng.choice([1e-3, 1e-6, 1e-2]))
+                kind = "hilbert" if rng.random() < 0.5 else "random"
+                path = "device" if rng.random() < 0.5 else "dropin"
+                max_itr = 60 if big else 200
             mat = orc.hilbert(n, dt) if kind == "hilbert" else orc.random_matrix(n, case, dt)
             if path == "dropin":
                 lam, v, _, itr, _ = ev.similarity_transform_ex(

@@ -23,7 +23,8 @@ new2)
 collect) python3 -m pytest --collect-only -q -m gpu tests/ > $O/collect.log 2>&1; tail -25 $O/collect.log ;;
 tests) run pytest_gpu 900 python3 -u -m pytest -x -q -rs --timeout 300 --timeout-method thread -m gpu tests/; tail -15 $O/pytest_gpu.log ;;
 smoke) run smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"; tail -3 $O/smoke.log ;;
-fuzz) run fuzz 900 python3 -u tools/fuzz_parity.py --cases ${FUZZ_CASES:-300} --seed ${FUZZ_SEED:-20261201} --json $O/r06_fuzz_parity.json; tail -3 $O/fuzz.log; grep -c STRADDLE $O/fuzz.log ;;
+fuzz) run fuzz 900 python3 -u tools/fuzz_parity.py --cases ${FUZZ_CASES:-300} --seed ${FUZZ_SEED:-20261201} --json $O/r06_fuzz_parity.json; tail -3 $O/fuzz.log; grep -c STRADDLE $O/fuzz.log || true ;;
+fuzzwrap) run fuzzwrap 900 python3 -u tools/fuzz_parity.py --profile wrapper --cases ${FUZZ_CASES:-200} --seed ${FUZZ_SEED:-20270202} --json $O/r06_fuzz_wrapper.json; tail -3 $O/fuzzwrap.log; grep -c STRADDLE $O/fuzzwrap.log || true ;;
 bench) run bench 900 python3 bench.py --steps 20 --warmup 5; tail -c 1500 $O/bench.log ;;
 benchquick) run benchquick 600 python3 bench.py --steps 20 --warmup 5 --no-cpu --no-north-star --no-headline; tail -c 2500 $O/benchquick.log ;;
 profdefault)
