@@ -1469,58 +1469,6 @@ k_parts_seg(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
   }
 }
 
-// k_parts_seg with one row per lane: the row's NS (16 or 32) partial slots
-// (those past ppr hold 0) summed in registers in the DPP tree's grouping -
-// pairs, quads, the quads of each 16 ((q0 + q1) + (q2 + q3)), then the two
-// 16s (NS = 32) - so each sum is bitwise k_parts_seg's (IEEE addition is
-// commutative, and the grouping is the tree's).  One wave per 64 rows
-// instead of 64 / NS rows: 16x / 32x fewer waves for the same loads.
-template <typename T, int NS>
-__device__ __forceinline__ T
-lane_tree16(const T* x)
-{
-  T q[4];
-#pragma unroll
-  for (int j = 0; j < 4; j++)
-    q[j] = (x[4 * j] + x[4 * j + 1]) + (x[4 * j + 2] + x[4 * j + 3]);
-  return (q[0] + q[1]) + (q[2] + q[3]);
-}
-
-template <typename T, int NS, int BLK = 64>
-__global__ __launch_bounds__(BLK) void
-k_parts_lane(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,
-             uint32_t ppr /* <= NS */, uint32_t k, const st_state* state,
-             const T* __restrict__ s_cur, T* __restrict__ v, uint32_t row0,
-             T* __restrict__ inv_next)
-{
-  static_assert(NS == 16 || NS == 32, "16 or 32 partial slots");
-  const uint32_t r = blockIdx.x * BLK + threadIdx.x;
-  if (r >= nrows)
-    return;
-  const uint32_t e = state != nullptr ? state->end : 0u; // no state: K0, ungated
-  T vr = (T)0, sr = (T)1, m = (T)1;
-  if (v != nullptr) {
-    vr = v[row0 + r];
-    sr = s_cur[row0 + r];
-    m = (T)state->max;
-  }
-  const T* row = part + (size_t)r * ppr;
-  T x[NS];
-#pragma unroll
-  for (int i = 0; i < NS; i++)
-    x[i] = (uint32_t)i < ppr ? row[i] : (T)0;
-  T t = lane_tree16<T, NS>(x);
-  if constexpr (NS == 32)
-    t = t + lane_tree16<T, NS>(x + 16);
-  if (e != 0 && e <= k)
-    return;
-  s_next[r] = t;
-  if (inv_next != nullptr)
-    inv_next[r] = (T)1 / t;
-  if (v != nullptr)
-    v[row0 + r] = vr * (sr / m); // cpp:260
-}
-
 template <typename T, int BLK = kBlock>
 __global__ __launch_bounds__(BLK) void
 k_parts(const T* __restrict__ part, T* __restrict__ s_next, uint32_t nrows,

@@ -340,28 +340,16 @@ every_cache_class(size_t bytes)
                                        : 3u;
 }
 
-// k_parts of an unsplit flat round: rows of <= 16 / 32 partials take one
-// lane each (k_parts_lane, g_parts_form 0) or 4 / 2 rows per wave
-// (k_parts_seg, 1) - both bitwise k_parts' sums - longer ones a wave each
-// (k_parts).  st_set_parts_form (tuning build) picks the form.
-std::atomic<uint32_t> g_parts_form{ 1u };
-
+// k_parts of an unsplit flat round: rows of <= 16 / 32 partials take 4 / 2
+// rows per wave (k_parts_seg, bitwise k_parts' sums), longer ones a wave
+// each (k_parts)
 template <typename T>
 void
 launch_parts(const T* part, T* s_next, uint32_t nrows, uint32_t ppr, uint32_t k,
              const st_state* st, const T* s_cur, T* v, uint32_t row0, T* inv_next,
              hipStream_t stream)
 {
-  const bool lane = g_parts_form.load(std::memory_order_relaxed) == 0u;
-  if (lane && ppr <= 32) {
-    const uint32_t g = (nrows + 63u) / 64u;
-    if (ppr <= 16)
-      hipLaunchKernelGGL((dev::k_parts_lane<T, 16>), dim3(g), dim3(64), 0, stream, part,
-                         s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next);
-    else
-      hipLaunchKernelGGL((dev::k_parts_lane<T, 32>), dim3(g), dim3(64), 0, stream, part,
-                         s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next);
-  } else if (ppr <= 16) {
+  if (ppr <= 16) {
     const uint32_t g = (nrows + kBlock / 16 - 1) / (kBlock / 16);
     hipLaunchKernelGGL((dev::k_parts_seg<T, 16>), dim3(g), dim3(kBlock), 0, stream, part,
                        s_next, nrows, ppr, k, st, s_cur, v, row0, inv_next);
@@ -2087,18 +2075,6 @@ st_every_cache_class(unsigned int nrows, unsigned int ncols, int dtype)
   }
   return (int)st::every_cache_class(
     st::block_bytes(nrows, ncols, dtype == 1 ? 8 : 4));
-}
-
-int
-st_set_parts_form(unsigned int form)
-{
-  st::clear_error();
-  if (form > 1u) {
-    st::set_error("st_set_parts_form: form %u (0 = a row per lane, 1 = rows of 16 / 32 "
-                  "lanes)", form);
-    return -1;
-  }
-  return (int)st::g_parts_form.exchange(form, std::memory_order_relaxed);
 }
 
 int

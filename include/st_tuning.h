@@ -40,12 +40,6 @@ unsigned int st_set_flat_grid_limit(unsigned int max_x);
  * and k_parts' order are fixed).  Returns the previous mode. */
 int st_set_k0_reverse(int mode);
 
-/* The flat round's second launch for rows of at most 32 partial sums:
- * 0 = one row per lane (k_parts_lane), 1 = rows of 16 / 32 lanes
- * (k_parts_seg).  Both give bitwise the same sums.  Returns the previous
- * form, or -1 (eigen_last_error) for another value. */
-int st_set_parts_form(unsigned int form);
-
 /* Workgroups per CU of the deferred flat round's launches (dtype 0 = f32,
  * 1 = f64; nontemporal = the launch form of blocks >= 2 GiB, else the cached
  * one; slot 0..4 = a read-only round with that many pending rounds, 6 =

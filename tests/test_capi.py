@@ -42,7 +42,7 @@ def test_product_library_exports_no_tuning_setter():
     st_set_* but the context's stream and the RCCL deadline."""
     exported = _exported(_lib.lib_path())
     tuning = _lib.declared_symbols(_lib.TUNING_HEADER)
-    assert len(tuning) == 12 and not (set(tuning) & exported), set(tuning) & exported
+    assert len(tuning) == 11 and not (set(tuning) & exported), set(tuning) & exported
     assert sorted(e for e in exported if e.startswith("st_set_")) == \
         ["st_set_comm_timeout", "st_set_stream"]
     assert not (exported - set(_lib.declared_symbols())), exported - set(_lib.declared_symbols())
@@ -61,9 +61,6 @@ def test_tuning_build_exports_the_tuning_abi():
     assert dflt in (-1, 0, 1) and L.st_set_k0_reverse(7) == 1
     assert L.st_set_k0_reverse(-5) == 1 and L.st_set_k0_reverse(0) == -1
     assert L.st_set_k0_reverse(dflt) == 0
-    form = L.st_set_parts_form(0)
-    assert form in (0, 1) and L.st_set_parts_form(2) < 0
-    assert "st_set_parts_form" in _lib.last_error(L) and L.st_set_parts_form(form) == 0
 
 
 def test_drop_in_signatures_are_c_abi():

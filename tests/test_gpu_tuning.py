@@ -250,46 +250,3 @@ else:
             assert dev.set_flat_grid_limit(0) == 16777208
         for x, y in zip(ref, got):
             assert (torch.equal(x, y) if isinstance(x, torch.Tensor) else x == y)
-
-
-    @pytest.mark.parametrize("dt,nrows,ncols", [(torch.float64, 4352, 4352), (torch.float64, 1031, 24100),
-                                                (torch.float32, 6151, 6152), (torch.float32, 1500, 40000),
-                                                (torch.float64, 7, 9000)])
-    def test_parts_forms_bitwise(solver, dt, nrows, ncols):
-        """The flat round's second launch for rows of <= 16 / 32 partials
-        (st_set_parts_form: a row per lane, or rows of 16 / 32 lanes) gives
-        the same row sums, v and 1/s bit for bit: one flat round of a row
-        block (v update), K0 (no state), and whole solves that defer writes
-        (1/s) or store every round.  The slot tree of k_parts_lane is the DPP
-        tree's grouping (st_device.h)."""
-        L = _lib.load()
-        g = torch.Generator().manual_seed(nrows + ncols)
-        a0 = (torch.rand(nrows, ncols, generator=g, dtype=torch.float64) + 0.01).to(dt).to(DEV)
-        s_cur = (torch.rand(ncols, generator=g, dtype=torch.float64) + 0.5).to(dt).to(DEV)
-        v0 = torch.rand(ncols, generator=g, dtype=torch.float64).to(dt).to(DEV)
-        ppr = int(L.st_round_flat_scratch(nrows, ncols)) // max(nrows, 1)
-        saved = L.st_set_parts_form(1)
-
-        def run():
-            a = a0.clone()
-            part = dev.flat_scratch(nrows, ncols, dt, DEV)
-            s0 = torch.empty(nrows, dtype=dt, device=DEV)
-            dev.rowsum_flat(a, s0, part)
-            s_next, v, st = torch.empty(nrows, dtype=dt, device=DEV), v0.clone(), dev.new_state(DEV)
-            dev.flat_round(a, s_cur, s_next, part, v, st, row0=min(3, ncols - nrows), eps=1e-3, k=2)
-            out = [s0.cpu(), a.cpu(), s_next.cpu(), v.cpu(), dev.read_state(st)]
-            if nrows == ncols:
-                for every in (False, True):
-                    r = solver.solve(a0, eps=0.0, max_itr=9, write_every_round=every)
-                    out += [r[0], r[2], r[1].cpu()]
-            return out
-
-        try:
-            ref = run()
-            assert L.st_set_parts_form(0) == 1
-            got = run()
-        finally:
-            L.st_set_parts_form(saved)
-        assert ppr <= 32, ppr
-        for x, y in zip(ref, got):
-            assert torch.equal(x, y) if isinstance(x, torch.Tensor) else x == y

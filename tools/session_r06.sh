@@ -60,12 +60,6 @@ everyab)
 k0order)
   # K0 walked front to back vs from the end on cacheable blocks (tuning build)
   EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run k0order 400 python3 -u tools/k0_order_probe.py --json $O/r06_k0_order.json; tail -8 $O/k0order.log ;;
-parts)
-  # the flat round's second launch: a row per lane vs rows of 16 / 32 lanes
-  # (tuning build): its knob test, then the A/B under a kernel trace
-  EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run parts_test 300 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_tuning.py -k parts_forms; tail -3 $O/parts_test.log
-  D=$O/partsprof; mkdir -p $D
-  EIGEN_VALUE_LIB=eigen_value_amd/lib/libsimilarity_transform_tuning.so run parts 400 rocprofv3 --kernel-trace --stats --output-format csv -d $D -o run -- python3 -u tools/parts_form_probe.py --json $O/r06_parts_form.json; tail -4 $O/parts.log; grep -E "k_parts" $D/run_kernel_stats.csv | cut -c1-160 ;;
 prefix)
   # the headline pass fresh and after each step bench.py runs before it
   run prefix 300 python3 -u tools/prefix_probe.py --json $O/r06_prefix_probe.json; cat $O/prefix.log | tail -12 ;;
