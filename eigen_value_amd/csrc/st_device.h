@@ -1,6 +1,6 @@
 // st_device.h — device code of the similarity-transform iteration for
-// gfx950 (CDNA4).  Included by st_kernels.hip (the library) and by
-// tools/tune_fused.hip (launch-shape sweeps); not a public header.
+// gfx950 (CDNA4).  Included by st_kernels.hip (the library; earlier
+// rounds' launch-shape sweeps are in the git history); not a public header.
 //
 // Reference behaviour (paths into itzmeanjan/eigen_value):
 //   sum_across_rows       similarity_transform.cpp:77-152
@@ -238,7 +238,7 @@ ld(const V* p)
 // loads it through the VECTOR memory path instead of a scalar load (whose
 // lgkmcnt wait - scalar loads return out of order, so a wave can only wait
 // for all of them - then also holds up the next kernel-argument pointer a
-// vector load needs).  Measured (tools/flat_map_sweep{,_vload},
+// vector load needs).  Measured (flat_map_sweep{,_vload} (round 2, git history),
 // profiles/r02_flat_map_rowload_*.log): 15-30 % SLOWER on non-temporal
 // fp64 blocks with pending rounds (32768^2, NP = 1: 1.62 vs 1.33 ms), equal
 // elsewhere, so the library keeps scalar row loads.
@@ -1119,7 +1119,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
   // scales of a vector without per-row conditions, so that the scalar loads
   // of adjacent rows merge (s_load_dwordx4 ... x16: one load and one address
   // per vector instead of R).  fp64 rounds with 1 - 4 pending scalings only
-  // (tools/flat_map_sweep A/B, profiles/r02_rowload_merge_ab*.log: 32768^2
+  // (flat_map_sweep (round 2, git history) A/B, profiles/r02_rowload_merge_ab*.log: 32768^2
   // NP = 4, 8 rows, tiles of 16: 1.23 vs 1.29 ms; the storing round with 5
   // pending and fp32 lose 1 - 2 %, their merged scales crowd the SGPRs)
   const T* rs = NP >= 0 ? pend.inv_cur : s_cur;

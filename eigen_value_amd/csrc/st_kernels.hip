@@ -89,8 +89,8 @@ check_launch(const char* what)
   return 0;
 }
 
-// Tuned shapes (tools/tune_fused.hip, tools/stream_bench.hip,
-// tools/sweep_dir.hip; profiles/README.md).  One 256-thread workgroup
+// Tuned shapes (the sweeps tune_fused.hip / sweep_dir.hip (git history),
+// tools/stream_bench.hip; profiles/README.md).  One 256-thread workgroup
 // streams a group of rows, 2 column chunks of 16 B per lane per row in
 // flight; the grid strides over the row groups.  What pays depends on the
 // size of the (local) matrix relative to the caches — 4 MB L2 per XCD, the
@@ -183,7 +183,7 @@ mfree_shape(uint32_t nrows, uint32_t ncols, size_t elem)
 // then serves the start of each round; odd rounds reverse the pieces in
 // steps of 8 workgroups so that every piece stays on its XCD and L2,
 // flat_reverse<2>) and non-temporal ones above:
-// tools/sweep_dir.hip SWEEP_FLAT=1 / SWEEP_XCD=1,
+// sweep_dir.hip (round 1, git history) SWEEP_FLAT=1 / SWEEP_XCD=1,
 // profiles/r01_sweep_flat_cached.log, r01_sweep_xcd{,_round}.log
 // (32768^2 fp64 2.68 ms vs 3.06 for k_round; 16384^2 0.67 vs 0.76; 8192^2
 // fp64 0.160 vs 0.168, fp32 0.079 vs 0.080; the 2880x23040 block 0.165 vs
@@ -253,7 +253,7 @@ template <typename T, int W, bool NT>
 constexpr int kFlatU =
   (W == 1 ? (int)(16 / sizeof(T)) : 1) * ((sizeof(T) == 8 && !NT) ? 2 : 1);
 
-// Shape of the every-round flat launch (tools/flat_map_sweep FMS_EVERY=1,
+// Shape of the every-round flat launch (flat_map_sweep (round 2, git history) FMS_EVERY=1,
 // profiles/r02_flat_map_every_*.log, two repeats each):
 //   non-temporal blocks  2 rows per workgroup, pieces walked in tiles of 4
 //                        row groups (32768^2 fp64 2.625 vs 2.688 ms, fp32
@@ -515,7 +515,7 @@ launch_split_rows(T* a, const T* s_cur, T* s_next, T* part, T* v,
   // the shape of the whole round (both halves stream the same rows); the
   // local half streams non-temporally so that it does not evict what the
   // remote half re-reads from the memory-side cache round after round
-  // (tools/sweep_dir.hip SWEEP_SPLIT=1: at the P = 8 block the pair then
+  // (sweep_dir.hip (round 1, git history) SWEEP_SPLIT=1: at the P = 8 block the pair then
   // costs 4 us over one k_round launch instead of 25 us)
   const Shape sh = round_shape(nrows, ncols, sizeof(T));
 #define ST_SPLIT_CFG(R, N)                                                     \
@@ -620,7 +620,7 @@ launch_mfree(const T* a0, const T* s_prev, T* s_next, const T* v_prev,
 // k_flat<..., MF> over one 4 / 8 KB piece of R rows per workgroup, the first
 // row group folding round k-1's stats, then k_mparts (s_k of the rows,
 // v_{k-1} of all n).  Same row sums up to association as k_mfree (pieces
-// summed apart).  Shapes (tools/store_probe SP_MF=1,
+// summed apart).  Shapes (store_probe (round 3, git history) SP_MF=1,
 // profiles/r03_mf_shapes_{nt,cached}.log; a flat launch + k_mparts against
 // one k_mfree launch): every lane's x = v ∘ s vector serves R rows, so 4 - 8
 // rows pay where the read-only deferred rounds take 1 - 2, and they want a
@@ -868,7 +868,7 @@ launch_round_flat(T* a, const T* s_cur, T* s_next, T* part, T* v,
 // (FlatPending in st_device.h): A is stored every defer_rounds() rounds;
 // the rounds in between re-apply the pending scalings from
 // the last stored matrix, bit-identical to storing every round.
-// tools/sweep_dir.hip SWEEP_DEFER=1 [SWEEP_DEFER_RING=1],
+// sweep_dir.hip (round 1, git history) SWEEP_DEFER=1 [SWEEP_DEFER_RING=1],
 // profiles/r01_sweep_defer{,_ring}.log, with s and 1/s in a ring of distinct
 // vectors as the solve keeps them: per round 32768^2 fp64 1.85 ms (every
 // 3rd round stored, 2 rows per workgroup) vs 2.70 storing every round,
@@ -912,7 +912,7 @@ launch_flat_deferred_np(T* a, const T* s_cur, const T* inv_cur, T* s_next,
 // flight oversubscribes the memory system at full occupancy (5-6
 // workgroups, up to 192 KB of loads per CU): capping it - with dynamic LDS
 // the kernel does not use, the only hard cap on workgroups per CU - is
-// faster: single launches (tools/store_probe SP_CAPS=1,
+// faster: single launches (store_probe (round 3, git history) SP_CAPS=1,
 // profiles/r03_store_probe_caps_*.log) the non-temporal storing round 2.85
 // -> 2.78 ms at 3 per CU (32768^2 fp64), NP = 3 1.205 -> 1.183 at 4; the
 // R = 2 launches (every-round, NP = 0) only lose.  The solve loop over whole
@@ -1006,7 +1006,7 @@ defer_lds(uint32_t slot)
 }
 
 // Launch shape of the deferred rounds by pending count NP
-// (tools/flat_map_sweep, profiles/r02_flat_map_shape_*.log and
+// (flat_map_sweep (round 2, git history), profiles/r02_flat_map_shape_*.log and
 // r02_flat_map_np5_*.log: 32768^2, 32768 / 16384 / 8192 x 65536 fp64
 // non-temporal, 8192^2 / 12288^2 / 2880 x 23040 fp64 cached, 32768^2 and
 // 8192^2 fp32):
