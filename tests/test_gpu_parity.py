@@ -619,6 +619,28 @@ def test_input_not_modified(eigen, orc):
     assert np.array_equal(mat, keep)       # similarity_transform.cpp:14,19
 
 
+def test_dropin_input_checks(eigen, orc, solver):
+    """What the reference's wrapper rejects, this one rejects the same way
+    (wrapper/python/similarity_transform.py:55-57: square, float32 - float64
+    added), and what it cannot express is an error, not a crash: an empty
+    matrix is a negative return with a message (the reference would divide
+    its work-group count by zero); a non-contiguous view is solved as its
+    C-contiguous copy; the device surface refuses a host tensor."""
+    with pytest.raises(AssertionError, match="square"):
+        eigen.similarity_transform(np.ones((3, 4), np.float32))
+    for bad in (np.int32, np.float16):
+        with pytest.raises(AssertionError, match="dtype"):
+            eigen.similarity_transform(np.ones((3, 3), bad))
+    with pytest.raises(ev.EigenValueError, match="dim must be > 0"):
+        eigen.similarity_transform(np.zeros((0, 0), np.float32))
+    mat = orc.random_matrix(130, 4, np.float32)
+    want = eigen.similarity_transform(mat)
+    got = eigen.similarity_transform(np.asfortranarray(mat))          # column-major
+    assert got[0] == want[0] and got[3] == want[3] and np.array_equal(got[1], want[1])
+    with pytest.raises(ValueError, match="HIP device"):
+        solver.solve(torch.from_numpy(mat))
+
+
 @pytest.mark.parametrize("dt", [np.float32, np.float64])
 @pytest.mark.parametrize("n", [1, 2, 3, 5, 17, 63, 65, 257])
 def test_edge_sizes(eigen, orc, dt, n):
