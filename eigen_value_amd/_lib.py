@@ -173,8 +173,6 @@ def declare_tuning(L: ctypes.CDLL) -> None:
     L.st_set_mfree_shape.restype = i32
     L.st_set_k0_reverse.argtypes = [i32]
     L.st_set_k0_reverse.restype = i32
-    L.st_set_every_late.argtypes = [u32, u32]
-    L.st_set_every_late.restype = i32
 
 
 def _declare(L: ctypes.CDLL) -> None:

@@ -950,8 +950,7 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
        uint32_t row0, uint32_t k, st_state* state, T eps = (T)0,
        uint32_t max_itr = 0, uint32_t semantics = 0, uint32_t p_lo = 0,
        uint32_t col0 = 0, uint32_t col1 = 0,
-       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0,
-       uint32_t late = 0xffffffffu)
+       FlatPending<T, NP> pend = FlatPending<T, NP>{}, uint32_t gx2 = 0)
 {
   constexpr int BLK = kBlock;
   // SPLIT (the overlapped exchange, sharded.py overlap=True): 1 = only the
@@ -1250,15 +1249,9 @@ k_flat(T* a, const T* __restrict__ s_cur, T* __restrict__ part,
           y = x[u][j] * (inv * sc[u]); // cpp:324-325
         else
           y = (inv * x[u][j]) * sc[u]; // main.py:13-16
-        if (do_store) {
-          // late: the workgroups dispatched from `late` on store with the
-          // other policy (uniform per workgroup)
-          V* dst = reinterpret_cast<V*>(a + (size_t)(r0 + j) * lda + c0 + u * BLK * W);
-          if (bl >= late)
-            st<V, !NTS>(dst, y);
-          else
-            st<V, NTS>(dst, y);
-        }
+        if (do_store)
+          st<V, NTS>(reinterpret_cast<V*>(a + (size_t)(r0 + j) * lda + c0 + u * BLK * W),
+                    y);
         acc[j] = u == 0 ? hsum<T, W>(y) : acc[j] + hsum<T, W>(y);
       }
     }

@@ -330,9 +330,6 @@ std::atomic<uint32_t> g_every_cache[kEveryCacheClasses] = { 2u, 2u, 0u, 0u };
 // as the registers allow; dynamic LDS the kernel does not use, as for the
 // deferred launches: defer_cap_lds), st_set_every_caps
 std::atomic<uint32_t> g_every_caps[kEveryCacheClasses] = { 0u, 0u, 0u, 0u };
-// per mille of the every-round launch's workgroups, the last ones dispatched,
-// whose stores take the other cache policy (0 = none; st_set_every_late)
-std::atomic<uint32_t> g_every_late[kEveryCacheClasses] = { 0u, 0u, 0u, 0u };
 
 inline uint32_t
 every_cache_class(size_t bytes)
@@ -795,17 +792,12 @@ launch_flat_parts(T* a, const T* s_cur, T* s_next, T* part, T* v,
     const uint32_t lds = defer_cap_lds(
       g_every_caps[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))].load(
         std::memory_order_relaxed));
-    const uint32_t late_pm =
-      g_every_late[every_cache_class(block_bytes(nrows, ncols, sizeof(T)))].load(
-        std::memory_order_relaxed);
-    const uint32_t late =
-      late_pm ? grid - (uint32_t)((uint64_t)grid * late_pm / 1000u) : 0xffffffffu;
 #define ST_EVERY(FL)                                                           \
   hipLaunchKernelGGL(                                                          \
     (dev::k_flat<T, W, ORDER, NT, R, true, kFlatAlt, 0, -1, U, -1, false,      \
                  FL>),                                                         \
     fg.grid, dim3(kBlock), lds, stream, a, s_cur, part, v, nrows, ncols, ppr,  \
-    row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2, late)
+    row0, k, st, eps, max_itr, semantics, 0u, 0u, 0u, pe, fg.gx2)
     constexpr int kV = W > 1 ? 1 : 0;
     switch (pol) {
       case 1u: ST_EVERY(kV); break;
@@ -2049,17 +2041,6 @@ st_set_every_caps(unsigned int size_class, unsigned int wg_per_cu)
   }
   return (int)st::g_every_caps[size_class].exchange(wg_per_cu,
                                                     std::memory_order_relaxed);
-}
-
-int
-st_set_every_late(unsigned int size_class, unsigned int per_mille)
-{
-  st::clear_error();
-  if (size_class >= (unsigned)st::kEveryCacheClasses || per_mille > 1000u) {
-    st::set_error("st_set_every_late: size class 0..3, 0..1000 per mille");
-    return -1;
-  }
-  return (int)st::g_every_late[size_class].exchange(per_mille, std::memory_order_relaxed);
 }
 
 int

@@ -40,12 +40,6 @@ unsigned int st_set_flat_grid_limit(unsigned int max_x);
  * and k_parts' order are fixed).  Returns the previous mode. */
 int st_set_k0_reverse(int mode);
 
-/* The every-round flat launch of a size class (st_every_cache_class): the
- * last per_mille / 1000 of its workgroups in dispatch order store with the
- * other cache policy (0 = none, the default).  Results do not depend on it.
- * Returns the previous value, or -1. */
-int st_set_every_late(unsigned int size_class, unsigned int per_mille);
-
 /* Workgroups per CU of the deferred flat round's launches (dtype 0 = f32,
  * 1 = f64; nontemporal = the launch form of blocks >= 2 GiB, else the cached
  * one; slot 0..4 = a read-only round with that many pending rounds, 6 =

@@ -42,7 +42,7 @@ def test_product_library_exports_no_tuning_setter():
     st_set_* but the context's stream and the RCCL deadline."""
     exported = _exported(_lib.lib_path())
     tuning = _lib.declared_symbols(_lib.TUNING_HEADER)
-    assert len(tuning) == 12 and not (set(tuning) & exported), set(tuning) & exported
+    assert len(tuning) == 11 and not (set(tuning) & exported), set(tuning) & exported
     assert sorted(e for e in exported if e.startswith("st_set_")) == \
         ["st_set_comm_timeout", "st_set_stream"]
     assert not (exported - set(_lib.declared_symbols())), exported - set(_lib.declared_symbols())

@@ -79,14 +79,12 @@ def set_every(policy, n, elem, nrows=None):
     from eigen_value_amd import _lib
     L = _lib.load()
     cls = L.st_every_cache_class(nrows or n, n, 1 if elem == 8 else 0)
-    # "P", "P:T", "P:T:C" or "P:T:C:L" (T: st_set_every_tile, C:
-    # st_set_every_caps, L: st_set_every_late, per mille)
-    pol, tile, cap, late = (policy.split(":") + ["", "", ""])[:4]
+    # "P", "P:T" or "P:T:C" (T: st_set_every_tile, C: st_set_every_caps)
+    pol, tile, cap = (policy.split(":") + ["", ""])[:3]
     old_pol = _lib.check(L.st_set_every_cache(cls, int(pol, 0)), "every_cache")
     old_tile = _lib.check(L.st_set_every_tile(cls, int(tile or "0", 0)), "every_tile")
     old_cap = _lib.check(L.st_set_every_caps(cls, int(cap or "0", 0)), "every_caps")
-    old_late = _lib.check(L.st_set_every_late(cls, int(late or "0", 0)), "every_late")
-    return f"{old_pol}:{old_tile}:{old_cap}:{old_late}"
+    return f"{old_pol}:{old_tile}:{old_cap}"
 
 
 def run_mfree_ab(args):
